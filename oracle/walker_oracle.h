@@ -1,0 +1,57 @@
+/* walker_oracle.h — CPU restatement of the reference walker step (TEST INFRASTRUCTURE ONLY).
+ *
+ * This is the checker, never the product: only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it.  See walker_oracle.c for the per-line reference citations.
+ * Layout: flat CSR over walkers (mass_off/edge_off/muscle_off, N+1 entries each); walker-local
+ * edge endpoints; muscles are the first (muscle_off[w+1]-muscle_off[w]) edges of walker w.
+ */
+#ifndef WALKER_ORACLE_H
+#define WALKER_ORACLE_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct orc_params {
+    double g, dampk, ground, groundk, grounddamp, friction, dt;
+    double pk, vk, ak, mk;
+    int32_t in3d, max_steps, midform, conmid;
+    int32_t spring_mode;   /* 0 = engine.py resilience + G2 damping; 1 = G2 optimized_walker as written */
+    int32_t action_mode;   /* 0 = Muscle.act (continuous); 1 = Muscle.actdisp (discrete) */
+} orc_params;
+
+typedef struct orc_batch {
+    int32_t N;
+    const int32_t *mass_off, *edge_off, *muscle_off;
+    float *pos, *vel, *acc;          /* [P*3] */
+    const float *m;                  /* [P]   */
+    const int32_t *ei, *ej;          /* [E] walker-local */
+    const float *rest, *k, *c;       /* [E]; rest of a muscle edge = its originx */
+    const uint8_t *flags;            /* [E] bit0 string (may be NULL) */
+    float *mx;                       /* [U] muscle rest length state */
+    const float *minl, *maxl, *stride; /* [U] */
+    int32_t *steps;                  /* [N] */
+    uint8_t *contact;                /* [P] (may be NULL) */
+} orc_batch;
+
+typedef struct orc_out {
+    float *obs; int32_t obs_stride;  /* [N*obs_stride] (may be NULL) */
+    float *reward; uint8_t *done; float *centroid; float *energy;  /* each may be NULL */
+} orc_out;
+
+int orc_abi_version(void);
+/* One env step for every walker: act -> springs -> env forces -> run1 -> observe. */
+int orc_step(const orc_batch *b, const orc_params *p, const float *action, int32_t action_cols,
+             int32_t action_stride, const orc_out *o, int32_t n_threads);
+/* Observation / reward / done / info for the current state (reset path; no physics). */
+int orc_observe(const orc_batch *b, const orc_params *p, const orc_out *o, int32_t n_threads);
+/* PhysicsEnv.reset: a = 0, v += noise (x,y; z if in3d), steps = 0. noise [P*3] (may be NULL). */
+int orc_reset(const orc_batch *b, const orc_params *p, const float *noise, int32_t n_threads);
+/* numpy float32 helpers exported for unit tests */
+float orc_np_norm3(const float *v);
+float orc_np_pairwise_sum(const float *a, int64_t n, int64_t stride);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

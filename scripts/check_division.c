@@ -1,0 +1,48 @@
+/* Host check of the exact-division identities the HIP kernel relies on (walker_hip.hip fdiv_exact /
+ * ddiv_exact): float x/m == (float)((double)x * RN64(1/m)) and Markstein's corrected double quotient.
+ * Usage: check_division [n]   (prints mismatch counts; all must be 0). */
+#include <stdio.h>
+#include <stdlib.h>
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+static uint64_t s=88172645463325252ull;
+static inline uint64_t xr(){ s^=s<<13; s^=s>>7; s^=s<<17; return s; }
+static float rf(){ // random float with random exponent in a physical range, random sign
+  uint32_t u = (uint32_t)xr();
+  int e = 127 + (int)(xr()%60) - 30;
+  u = (u & 0x807fffffu) | ((uint32_t)e<<23);
+  float f; memcpy(&f,&u,4); return f;
+}
+static double rd(){ uint64_t u=xr(); int e=1023+(int)(xr()%80)-40; u=(u&0x800fffffffffffffull)|((uint64_t)e<<52); double d; memcpy(&d,&u,8); return d; }
+int main(int argc, char** argv){
+  long bad1=0,bad2=0,bad3=0,n=argc>1?atol(argv[1]):200000000;
+  for(long i=0;i<n;i++){
+    // (1) f32 x / f32 m exact via double reciprocal
+    float x=rf(), m=fabsf(rf());
+    double ym = 1.0/(double)m;
+    float q1 = (float)((double)x*ym);
+    if (q1 != x/m) bad1++;
+    // (2) double t / f32-valued double m, Markstein with y = RN(1/m)
+    double t = rd(); double md=(double)m;
+    double q = t*ym; double r = fma(-q, md, t); double q2 = fma(r, ym, q);
+    if (q2 != t/md) bad2++;
+    // (3) double (f32 value) / f32 cur (the spring t = fv/dist)
+    double fv=(double)rf(); double c=(double)fabsf(rf()); double yc=1.0/c;
+    double qq = fv*yc; double rr=fma(-qq,c,fv); double q3=fma(rr,yc,qq);
+    if (q3 != fv/c) bad3++;
+  }
+  printf("n=%ld bad f32-via-f64=%ld markstein(t/m)=%ld markstein(fv/c)=%ld\n", n, bad1, bad2, bad3);
+  // adversarial: m with all-ones mantissa, t near multiples
+  long b4=0;
+  for (long i=0;i<n/4;i++){
+    uint32_t u = 0x3f800000u | (0x7fffffu - (uint32_t)(xr()%64)); float m; memcpy(&m,&u,4);
+    double t = (double)(int64_t)(xr()>>11) * ldexp(1.0, -(int)(xr()%60));
+    double ym=1.0/(double)m; double q=t*ym; double r=fma(-q,(double)m,t); double q2=fma(r,ym,q);
+    if (q2 != t/(double)m) b4++;
+    float x; uint32_t ux = (uint32_t)xr() & 0x7fffffffu; if (((ux>>23)&0xff)==0xff || ((ux>>23)&0xff)==0) continue; memcpy(&x,&ux,4);
+    if ((float)((double)x*ym) != x/m) b4++;
+  }
+  printf("adversarial bad=%ld\n", b4);
+  return (bad1||bad2||bad3||b4) ? 1 : 0;
+}

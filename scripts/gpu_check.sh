@@ -1,0 +1,19 @@
+#!/bin/bash
+# GPU session: parity tests, smoke, bench, rocprof kernel trace.  Each GPU step has its own time
+# limit; a crash/abort/timeout (rc >= 124) ends the session; plain test failures (rc 1) do not.
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {  # step <name> <timeout_s> <cmd...>
+  local name=$1 t=$2; shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "   rc=$rc"; tail -n 5 "gpurun_out/$name.log"
+  if [ $rc -ge 2 ] && [ $rc -ne 5 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+step pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider -x
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step bench 600 python bench.py --steps 300 --warmup 30
+step rocprof_trace 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 200 --warmup 20 --no-cpu-baseline

@@ -1,0 +1,95 @@
+"""ctypes binding of libwalker_hip.so (the C ABI in include/walker_hip.h).
+
+The library is built in-tree (walker_gym_amd/libwalker_hip.so, see walker_gym_amd/build.py) so it
+travels with the repo to the GPU box.  There is no fallback: if the library is missing or its ABI
+version differs, every entry point raises — the product never silently runs on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_NAME = "libwalker_hip.so"
+LIB_PATH = os.path.join(HERE, LIB_NAME)
+ABI_VERSION = 1
+
+WG_EINVAL, WG_ERANGE, WG_EHIP = -1, -2, -3
+
+_vp = C.c_void_p
+
+
+class WgParams(C.Structure):
+    _fields_ = [(n, C.c_double) for n in ("g", "dampk", "ground", "groundk", "grounddamp", "friction", "dt",
+                                           "pk", "vk", "ak", "mk")] + \
+               [(n, C.c_int32) for n in ("in3d", "max_steps", "midform", "conmid", "spring_mode", "action_mode")]
+
+
+class WgBatch(C.Structure):
+    _fields_ = [("N", C.c_int32), ("M", C.c_int32), ("K", C.c_int32), ("A", C.c_int32),
+                ("ragged", C.c_int32),
+                ("mass_off", _vp), ("edge_off", _vp), ("muscle_off", _vp),
+                ("pos", _vp), ("vel", _vp), ("acc", _vp), ("mass", _vp),
+                ("edge_ij", _vp), ("edge_rest", _vp), ("edge_k", _vp), ("edge_c", _vp), ("edge_flags", _vp),
+                ("inc", _vp), ("inc_off", _vp),
+                ("muscle_x", _vp), ("muscle_lo", _vp), ("muscle_hi", _vp), ("muscle_stride", _vp),
+                ("steps", _vp), ("contact", _vp)]
+
+
+class WgOutputs(C.Structure):
+    _fields_ = [("obs", _vp), ("obs_stride", C.c_int32), ("reward", _vp), ("done", _vp),
+                ("centroid", _vp), ("energy", _vp), ("obs_step", C.c_int64), ("out_step", C.c_int64)]
+
+
+class WgLaunchInfo(C.Structure):
+    _fields_ = [("threads", C.c_int32), ("walkers_per_block", C.c_int32), ("blocks", C.c_int32),
+                ("lds_bytes", C.c_int32)]
+
+
+EXPORTS = ("wg_abi_version", "wg_last_error", "wg_step", "wg_observe", "wg_reset", "wg_plan_ragged",
+           "wg_launch_geometry")
+
+_lib = None
+_lock = threading.Lock()
+
+
+class WalkerHipError(RuntimeError):
+    pass
+
+
+def load(path: str | None = None):
+    """Load (once) and type the library. Raises if it is missing or has the wrong ABI version."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        p = path or os.environ.get("WALKER_HIP_LIB", LIB_PATH)
+        if not os.path.exists(p):
+            raise WalkerHipError(
+                f"{p} not found: build it with `python -m walker_gym_amd.build` (hipcc --offload-arch=gfx950); "
+                "walker_gym_amd has no CPU fallback")
+        L = C.CDLL(p)
+        L.wg_abi_version.restype = C.c_int
+        L.wg_last_error.restype = C.c_char_p
+        L.wg_step.argtypes = [C.POINTER(WgBatch), C.POINTER(WgParams), _vp, C.c_int32, C.c_int32, C.c_int64,
+                              C.POINTER(WgOutputs), C.c_int32, _vp, C.c_int32, _vp]
+        L.wg_observe.argtypes = [C.POINTER(WgBatch), C.POINTER(WgParams), C.POINTER(WgOutputs), _vp, C.c_int32, _vp]
+        L.wg_reset.argtypes = [C.POINTER(WgBatch), C.POINTER(WgParams), _vp, _vp, _vp]
+        L.wg_plan_ragged.argtypes = [_vp, _vp, _vp, C.c_int32, _vp, C.c_int32]
+        L.wg_launch_geometry.argtypes = [C.POINTER(WgBatch), C.POINTER(WgLaunchInfo)]
+        for f in ("wg_step", "wg_observe", "wg_reset", "wg_plan_ragged", "wg_launch_geometry"):
+            getattr(L, f).restype = C.c_int
+        v = L.wg_abi_version()
+        if v != ABI_VERSION:
+            raise WalkerHipError(f"{p}: ABI version {v}, expected {ABI_VERSION}")
+        _lib = L
+        return L
+
+
+def check(rc: int, what: str) -> int:
+    if rc < 0:
+        msg = load().wg_last_error().decode(errors="replace")
+        exc = ValueError if rc in (WG_EINVAL, WG_ERANGE) else WalkerHipError
+        raise exc(f"{what}: {msg} (code {rc})")
+    return rc

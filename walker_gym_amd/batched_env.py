@@ -1,0 +1,222 @@
+"""BatchedPhysicsEnv — N independent walkers stepped by one HIP launch per env step.
+
+The batched form of the reference's gym-style API (gym/optimized_env.py:8-269):
+  reset(noise=None, mask=None)        -> obs [N, D]                     (PhysicsEnv.reset :53-68)
+  step(action [N, A])                 -> obs, reward [N], done [N], info (PhysicsEnv.step :70-92)
+  rollout(actions [T, N, A])          -> obs [T, N, D], reward [T, N], done [T, N]   (one C call)
+  observe()                           -> obs, reward, done, info for the current state
+Environment parameters keep the reference's names and defaults (PhysicsEnv.__init__ :15-17).
+obs rows are Creature.getstat (gym/optimized_walker.py:129-162), zero-padded to D = max row length
+for ragged batches (``obs_len`` gives each walker's length).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, asdict
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from .device import DeviceBatch
+from .layout import HostLayout, pack
+
+
+@dataclass
+class EnvParams:
+    """PhysicsEnv / Environment constructor parameters + getstat options (reference defaults)."""
+    g: float = 100.0
+    dampk: float = 0.0
+    ground: float = 0.0           # ground_high / groundhigh
+    groundk: float = 1000.0       # ground_k
+    grounddamp: float = 100.0     # ground_damp
+    friction: float = 100.0
+    dt: float = 0.01              # PhysicsEnv.time_step (optimized_env.py:42)
+    in3d: bool = False
+    max_steps: int = 1000         # optimized_env.py:44
+    pk: float = 1.0
+    vk: float = 1.0
+    ak: float = 1.0
+    mk: float = 1.0
+    midform: bool = True
+    conmid: bool = False
+    spring_mode: int = 0          # 0: engine.py resilience + damping; 1: G2 optimized_walker as written
+    action_mode: int = 0          # 0: Muscle.act; 1: Muscle.actdisp
+
+    def to_struct(self) -> _lib.WgParams:
+        d = asdict(self)
+        return _lib.WgParams(**{k: (int(v) if k in ("in3d", "max_steps", "midform", "conmid", "spring_mode",
+                                                    "action_mode") else float(v)) for k, v in d.items()})
+
+
+class BatchedPhysicsEnv:
+    def __init__(self, spec_or_layout, device=None, rand_sigma: float = 0.0, seed: Optional[int] = None,
+                 contact: bool = True, **params):
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else None
+        if device is None:
+            raise RuntimeError("BatchedPhysicsEnv needs a ROCm GPU (libwalker_hip.so); there is no CPU path")
+        device = torch.device(device)
+        _lib.load()   # fail loudly before allocating anything
+        self.params = EnvParams(**params)
+        self.sigma = float(rand_sigma)
+        host = spec_or_layout if isinstance(spec_or_layout, HostLayout) else pack(spec_or_layout)
+        self.batch = DeviceBatch(host, device, contact=contact)
+        self.device = device
+        self.N = host.N
+        self.obs_len = host.obs_len(self.params.in3d, self.params.conmid)
+        self.obs_dim = int(self.obs_len.max())
+        self._pstruct = self.params.to_struct()
+        self._gen = torch.Generator(device=device)
+        if seed is not None:
+            self._gen.manual_seed(int(seed))
+        self._alloc_outputs()
+
+    # ------------------------------------------------------------------ plumbing
+    def _alloc_outputs(self):
+        N, D, dv = self.N, self.obs_dim, self.device
+        self.obs = torch.zeros((N, D), dtype=torch.float32, device=dv)
+        self.reward = torch.zeros(N, dtype=torch.float32, device=dv)
+        self.done = torch.zeros(N, dtype=torch.uint8, device=dv)
+        self.centroid = torch.zeros((N, 3), dtype=torch.float32, device=dv)
+        self.energy = torch.zeros(N, dtype=torch.float32, device=dv)
+
+    def _outputs(self, obs=None, reward=None, done=None, centroid=None, energy=None, obs_step=0, out_step=0):
+        p = lambda t: None if t is None else C.c_void_p(t.data_ptr())
+        return _lib.WgOutputs(obs=p(obs), obs_stride=self.obs_dim, reward=p(reward), done=p(done),
+                              centroid=p(centroid), energy=p(energy), obs_step=obs_step, out_step=out_step)
+
+    def _stream(self):
+        return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def set_params(self, **kw):
+        for k, v in kw.items():
+            if not hasattr(self.params, k):
+                raise AttributeError(k)
+            setattr(self.params, k, v)
+        self.obs_len = self.batch.host.obs_len(self.params.in3d, self.params.conmid)
+        if int(self.obs_len.max()) != self.obs_dim:
+            self.obs_dim = int(self.obs_len.max())
+            self._alloc_outputs()
+        self._pstruct = self.params.to_struct()
+
+    def _check_action(self, action):
+        if action is None:
+            return None, 0
+        if not isinstance(action, torch.Tensor):
+            action = torch.as_tensor(np.asarray(action, dtype=np.float32))
+        action = action.to(self.device, torch.float32)
+        if action.dim() == 1 and self.N == 1:
+            action = action[None]
+        if action.dim() != 2 or action.shape[0] != self.N:
+            raise ValueError(f"action must be [N={self.N}, A], got {tuple(action.shape)}")
+        return action.contiguous(), action.shape[1]
+
+    # ------------------------------------------------------------------ API
+    def step(self, action=None):
+        """One env step for all walkers: act -> physics -> run1 -> obs/reward/done/info (one launch)."""
+        act, cols = self._check_action(action)
+        L = _lib.load()
+        o = self._outputs(self.obs, self.reward, self.done, self.centroid, self.energy)
+        _lib.check(L.wg_step(C.byref(self.batch.struct), C.byref(self._pstruct),
+                             None if act is None else C.c_void_p(act.data_ptr()), cols, cols, 0, C.byref(o), 1,
+                             None if self.batch.plan is None else C.c_void_p(self.batch.plan.data_ptr()),
+                             self.batch.plan_blocks, self._stream()), "wg_step")
+        return self.obs, self.reward, self.done.bool(), self.info()
+
+    def rollout(self, actions, obs_out=None, reward_out=None, done_out=None):
+        """T steps in one C call (T back-to-back launches, no host sync); outputs for every step."""
+        if not isinstance(actions, torch.Tensor):
+            actions = torch.as_tensor(np.asarray(actions, dtype=np.float32))
+        actions = actions.to(self.device, torch.float32).contiguous()
+        if actions.dim() != 3 or actions.shape[1] != self.N:
+            raise ValueError("actions must be [T, N, A]")
+        T, _, cols = actions.shape
+        dv = self.device
+        obs_out = torch.empty((T, self.N, self.obs_dim), dtype=torch.float32, device=dv) if obs_out is None else obs_out
+        reward_out = torch.empty((T, self.N), dtype=torch.float32, device=dv) if reward_out is None else reward_out
+        done_out = torch.empty((T, self.N), dtype=torch.uint8, device=dv) if done_out is None else done_out
+        o = self._outputs(obs_out, reward_out, done_out, None, None, obs_step=self.N * self.obs_dim,
+                          out_step=self.N)
+        _lib.check(_lib.load().wg_step(
+            C.byref(self.batch.struct), C.byref(self._pstruct), C.c_void_p(actions.data_ptr()), cols, cols,
+            self.N * cols, C.byref(o), T,
+            None if self.batch.plan is None else C.c_void_p(self.batch.plan.data_ptr()),
+            self.batch.plan_blocks, self._stream()), "wg_step")
+        return obs_out, reward_out, done_out
+
+    def run(self, actions, n_steps: int, info: bool = True):
+        """Throughput path: n_steps env steps in one C call; step s acts with actions[s % T]
+        ([T, N, A] device tensor; T == n_steps or 1) and overwrites obs/reward/done(/info) each step."""
+        T, n, cols = actions.shape
+        if n != self.N or T not in (1, n_steps) or not actions.is_contiguous():
+            raise ValueError("actions must be a contiguous [n_steps or 1, N, A] device tensor")
+        o = self._outputs(self.obs, self.reward, self.done, self.centroid if info else None,
+                          self.energy if info else None)
+        _lib.check(_lib.load().wg_step(
+            C.byref(self.batch.struct), C.byref(self._pstruct), C.c_void_p(actions.data_ptr()), cols, cols,
+            0 if T == 1 else self.N * cols, C.byref(o), int(n_steps),
+            None if self.batch.plan is None else C.c_void_p(self.batch.plan.data_ptr()),
+            self.batch.plan_blocks, self._stream()), "wg_step")
+
+    def observe(self):
+        o = self._outputs(self.obs, self.reward, self.done, self.centroid, self.energy)
+        _lib.check(_lib.load().wg_observe(
+            C.byref(self.batch.struct), C.byref(self._pstruct), C.byref(o),
+            None if self.batch.plan is None else C.c_void_p(self.batch.plan.data_ptr()),
+            self.batch.plan_blocks, self._stream()), "wg_observe")
+        return self.obs, self.reward, self.done.bool(), self.info()
+
+    def reset(self, noise=None, mask=None):
+        """PhysicsEnv.reset: v += N(0, sigma) noise on x, y (and z if in3d); steps = 0; returns obs.
+        ``noise`` [P, 3] overrides the device generator (use it for reproducible parity runs)."""
+        if noise is None and self.sigma > 0:
+            noise = torch.randn((self.batch.P, 3), generator=self._gen, device=self.device) * self.sigma
+        if noise is not None:
+            noise = torch.as_tensor(noise, dtype=torch.float32).to(self.device).reshape(self.batch.P, 3).contiguous()
+        if mask is not None:
+            mask = torch.as_tensor(mask).to(self.device, torch.uint8).contiguous()
+        _lib.check(_lib.load().wg_reset(
+            C.byref(self.batch.struct), C.byref(self._pstruct),
+            None if noise is None else C.c_void_p(noise.data_ptr()),
+            None if mask is None else C.c_void_p(mask.data_ptr()), self._stream()), "wg_reset")
+        return self.observe()[0]
+
+    def seed(self, seed: Optional[int] = None) -> Sequence[int]:
+        if seed is not None:
+            self._gen.manual_seed(int(seed))
+        return [seed] if seed is not None else []
+
+    def info(self) -> dict:
+        return {"steps": self.batch.steps, "centroid_position": self.centroid, "total_energy": self.energy}
+
+    # state accessors (device tensors, views into the batch)
+    @property
+    def pos(self):
+        return self.batch.pos
+
+    @property
+    def vel(self):
+        return self.batch.vel
+
+    @property
+    def acc(self):
+        return self.batch.acc
+
+    @property
+    def muscle_x(self):
+        return self.batch.muscle_x
+
+    @property
+    def contact(self):
+        return self.batch.contact
+
+    def get_action_space(self) -> dict:
+        return {"shape": (self.batch.A,), "type": "continuous", "low": -1.0, "high": 1.0}
+
+    def get_observation_space(self) -> dict:
+        return {"shape": (self.obs_dim,), "type": "continuous", "low": -np.inf, "high": np.inf}
+
+    def launch_geometry(self) -> dict:
+        return self.batch.launch_geometry()

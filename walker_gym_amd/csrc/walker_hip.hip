@@ -1,0 +1,816 @@
+// walker_hip.hip — MI355X (gfx950 / CDNA4) batched walker stepper + the C ABI of include/walker_hip.h.
+//
+// One launch = one env step for every walker:
+//   act (Muscle.act/regulation)  ->  springs in edge order  ->  gravity, damp, ground  ->
+//   symplectic Euler (Point.run1)  ->  observation, reward, done, info.
+//
+// Execution model:
+//   * a workgroup owns a CONTIGUOUS range of walkers, so every SoA array it touches is one contiguous
+//     byte range in HBM.  Phase 0 issues EVERY global load of the tile back to back (state -> LDS with
+//     16-B loads; edge / muscle / incidence-offset records -> registers of the lane that uses them),
+//     so the tile pays one HBM latency, not a chain of them;
+//   * act: muscle lanes update the rest lengths straight from registers;
+//   * edge phase: one lane per edge computes the spring term t = RN64(f*dir / dist) and the damping
+//     force df (float32) ONCE, into LDS;
+//   * mass phase: one lane per mass walks its incidence list (LDS, sorted by edge index) and
+//     accumulates a = f32(f64(a) + t/m) then a += df/m in exactly the reference's order, then env
+//     forces and the integrator in registers — deterministic, no atomics;
+//   * observe: per-walker reductions in numpy's summation order (8 lanes per walker), obs rows written
+//     as one contiguous coalesced block.
+// Compiled with -ffp-contract=off and IEEE f32/f64 division/sqrt (build.py), so each float op rounds
+// exactly as numpy's does.
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+
+#include "walker_hip.h"
+
+namespace {
+
+thread_local char g_err[512] = "";
+
+int fail(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+constexpr int WG_MAX_M = 1024;      // numpy pairwise recursion unrolled 3 levels (pw_tree<3>)
+constexpr double CONFIG_R = 16e-36;  // gym/engine.py:9 Config.r (distance clamp, Python float)
+constexpr int EPL = 4;               // edges per lane per pass held in registers
+constexpr int NTHREADS = 256;
+#ifndef WG_ABLATE
+#define WG_ABLATE 0   // profiling builds only (scripts/ablate.py): bit k skips phase k; 0 in the product
+#endif
+
+// Float32 constants derived from wg_params exactly where numpy rounds the Python scalars.
+struct KParams {
+    float neg_g, neg_dampk, ground, neg_groundk, neg_grounddamp, friction, dt;
+    float pk, vk, ak, mk, done_y;
+    double g;
+    int max_steps, midform, conmid, spring_mode, action_mode;
+};
+
+// Per-launch geometry: caps of one workgroup's slice (LDS carve sizes).
+struct Geo {
+    int W, Pcap, Ecap, Ucap;   // walkers, masses, edges, muscles per workgroup (max)
+    int threads;
+    int lds;
+    float invM, invK, invA;    // uniform batches: 1/M, 1/K, 1/A for exact small-int division (fdiv)
+    int tbytes;                // spring-term region, also the obs tile of uniform batches (aliased)
+};
+
+struct Carve {
+    double *t;                   // [Ecap*3] spring term RN64(f*dir/dist)
+    float *pos, *vel, *acc, *m;  // [Pcap*3] / [Pcap]
+    float *df;                   // [Ecap*3] damping force
+    uint32_t *inc;               // [Ecap]   incidence entries, two u16 per word
+    float *x;                    // [Ucap]   muscle rest length after act
+    float *nrm, *ke, *pe;        // [Pcap]   per-mass reduction terms
+    float *red;                  // [W*8]    per-walker reductions
+    int *moff, *eoff, *uoff;     // [W+1]    block-local walker offsets (ragged)
+};
+
+__host__ __device__ inline int align16(int b) { return (b + 15) & ~15; }
+
+__host__ __device__ inline int carve_bytes(const Geo &g) {
+    return align16(g.tbytes) + 3 * align16(g.Pcap * 3 * 4) + align16(g.Pcap * 4) +
+           align16(g.Ecap * 3 * 4) + align16(g.Ecap * 4 + 16) + align16(g.Ucap * 4) + 3 * align16(g.Pcap * 4) +
+           align16(g.W * 8 * 4) + 3 * align16((g.W + 1) * 4);
+}
+
+__device__ inline Carve carve(char *s, const Geo &g) {
+    Carve c;
+    int b = 0;
+    c.t = reinterpret_cast<double *>(s + b); b += align16(g.tbytes);
+    c.pos = reinterpret_cast<float *>(s + b); b += align16(g.Pcap * 3 * 4);
+    c.vel = reinterpret_cast<float *>(s + b); b += align16(g.Pcap * 3 * 4);
+    c.acc = reinterpret_cast<float *>(s + b); b += align16(g.Pcap * 3 * 4);
+    c.m = reinterpret_cast<float *>(s + b); b += align16(g.Pcap * 4);
+    c.df = reinterpret_cast<float *>(s + b); b += align16(g.Ecap * 3 * 4);
+    c.inc = reinterpret_cast<uint32_t *>(s + b); b += align16(g.Ecap * 4 + 16);
+    c.x = reinterpret_cast<float *>(s + b); b += align16(g.Ucap * 4);
+    c.nrm = reinterpret_cast<float *>(s + b); b += align16(g.Pcap * 4);
+    c.ke = reinterpret_cast<float *>(s + b); b += align16(g.Pcap * 4);
+    c.pe = reinterpret_cast<float *>(s + b); b += align16(g.Pcap * 4);
+    c.red = reinterpret_cast<float *>(s + b); b += align16(g.W * 8 * 4);
+    c.moff = reinterpret_cast<int *>(s + b); b += align16((g.W + 1) * 4);
+    c.eoff = reinterpret_cast<int *>(s + b); b += align16((g.W + 1) * 4);
+    c.uoff = reinterpret_cast<int *>(s + b); b += align16((g.W + 1) * 4);
+    return c;
+}
+
+// ------------------------------------------------------------------ numpy-exact float helpers
+// np.linalg.norm of a float32 3-vector: OpenBLAS sdot (float products summed in double), float sqrt.
+__device__ inline float np_norm3(float x, float y, float z) {
+    const float px = x * x, py = y * y, pz = z * z;
+    double s = 0.0;
+    s += (double)px; s += (double)py; s += (double)pz;
+    return sqrtf((float)s);
+}
+__device__ inline float np_dot3(float ax, float ay, float az, float bx, float by, float bz) {
+    const float p0 = ax * bx, p1 = ay * by, p2 = az * bz;
+    double s = 0.0;
+    s += (double)p0; s += (double)p1; s += (double)p2;
+    return (float)s;
+}
+// numpy float32 pairwise summation (the add.reduce inner loop behind np.mean / np.sum) over a
+// strided LDS array: < 8 sequential; <= 128 eight interleaved partial sums; above that numpy
+// recurses on halves split at a multiple of 8.
+__device__ inline float pw_leaf(const float *a, int n, int st) {
+    if (n < 8) {
+        float r = 0.f;
+        for (int i = 0; i < n; i++) r += a[i * st];
+        return r;
+    }
+    float r0 = a[0], r1 = a[st], r2 = a[2 * st], r3 = a[3 * st];
+    float r4 = a[4 * st], r5 = a[5 * st], r6 = a[6 * st], r7 = a[7 * st];
+    int i = 8;
+    for (; i < n - (n % 8); i += 8) {
+        const float *p = a + i * st;
+        r0 += p[0]; r1 += p[st]; r2 += p[2 * st]; r3 += p[3 * st];
+        r4 += p[4 * st]; r5 += p[5 * st]; r6 += p[6 * st]; r7 += p[7 * st];
+    }
+    float res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+    for (; i < n; i++) res += a[i * st];
+    return res;
+}
+template <int D>
+__device__ inline float pw_tree(const float *a, int n, int st) {
+    if (D == 0 || n <= 128) return pw_leaf(a, n, st);
+    int n2 = n / 2;
+    n2 -= n2 % 8;
+    return pw_tree<(D > 0 ? D - 1 : 0)>(a, n2, st) + pw_tree<(D > 0 ? D - 1 : 0)>(a + n2 * st, n - n2, st);
+}
+// PWD = recursion levels unrolled: 0 covers n <= 128 (the common kernel), 3 covers n <= 1024.
+template <int PWD>
+__device__ inline float np_pairwise(const float *a, int n, int st) { return pw_tree<PWD>(a, n, st); }
+
+__device__ inline int locate(const int *off, int n, int x) {  // largest w with off[w] <= x, w < n
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (off[mid] <= x) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+// exact idx / d for 0 <= idx < 2^24 via a float reciprocal and one correction
+__device__ inline int fdiv(int idx, int d, float inv) {
+    int q = (int)((float)idx * inv);
+    if (q * d > idx) q--;
+    else if ((q + 1) * d <= idx) q++;
+    return q;
+}
+
+// ---- exact IEEE quotients from one precomputed reciprocal (validated exhaustively-random on the host,
+// scripts/check_division.c):
+//  * float x / float m  ==  (float)((double)x * RN64(1/m))   for every normal quotient: the double
+//    product is within 2^-52 relative of x/m, and a quotient of two 24-bit floats cannot lie that close
+//    to a float rounding midpoint without being on it (it cannot be on it: it would need 25 bits);
+//  * double a / double b == fma(fma(-q, b, a), y, q) with y = RN64(1/b), q = RN64(a*y)  (Markstein's
+//    final correction step: y within 1/2 ulp of 1/b and q within 1 ulp of a/b -> correctly rounded).
+// Non-finite operands take the plain expression (the correction would turn inf into NaN).
+__device__ inline float fdiv_exact(float x, double y) { return (float)((double)x * y); }
+__device__ inline double ddiv_exact(double a, double b, double y) {
+    const double q = a * y;
+    if (!__builtin_isfinite(q) || y == 0.0) return q;
+    return __builtin_fma(__builtin_fma(-q, b, a), y, q);
+}
+
+// Global -> LDS copy of n 4-byte words (16-B vector loads when both ends allow it).
+template <typename T4, typename T1>
+__device__ inline void stage_in(T1 *dst, const T1 *__restrict__ src, int n, int tid) {
+    if ((((uintptr_t)src) & 15) == 0 && (n & 3) == 0) {
+        const T4 *s4 = reinterpret_cast<const T4 *>(src);
+        T4 *d4 = reinterpret_cast<T4 *>(dst);
+        for (int i = tid; i < (n >> 2); i += NTHREADS) d4[i] = s4[i];
+    } else {
+        for (int i = tid; i < n; i += NTHREADS) dst[i] = src[i];
+    }
+}
+__device__ inline void stage_out(float *__restrict__ dst, const float *src, int n, int tid) {
+    if ((((uintptr_t)dst) & 15) == 0 && (n & 3) == 0) {
+        const float4 *s4 = reinterpret_cast<const float4 *>(src);
+        float4 *d4 = reinterpret_cast<float4 *>(dst);
+        for (int i = tid; i < (n >> 2); i += NTHREADS) d4[i] = s4[i];
+    } else {
+        for (int i = tid; i < n; i += NTHREADS) dst[i] = src[i];
+    }
+}
+
+struct EdgeRec { uint32_t ij; float rest, k, c; uint32_t flag; };
+
+// ------------------------------------------------------------------ the step kernel
+// STEP = false: observe only (reset path).  RAGGED: CSR offsets + block plan.  IN3D: obs layout.
+template <bool STEP, bool RAGGED, bool IN3D, int PWD>
+__global__ __launch_bounds__(NTHREADS) void walker_step_kernel(
+    wg_batch b, KParams kp, const float *__restrict__ action, int action_cols, int action_stride,
+    wg_outputs o, const int32_t *__restrict__ plan, Geo geo) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    Carve s = carve(smem, geo);
+    const int tid = threadIdx.x;
+
+    // ---- this workgroup's walker range and flat slices
+    int w0, w1;
+    if (RAGGED) { w0 = plan[blockIdx.x]; w1 = plan[blockIdx.x + 1]; }
+    else { w0 = blockIdx.x * geo.W; w1 = min(w0 + geo.W, b.N); }
+    const int nw = w1 - w0;
+    int P0, P1, E0, E1, U0, U1;
+    if (RAGGED) {
+        P0 = b.mass_off[w0]; P1 = b.mass_off[w1];
+        E0 = b.edge_off[w0]; E1 = b.edge_off[w1];
+        U0 = b.muscle_off[w0]; U1 = b.muscle_off[w1];
+        for (int i = tid; i <= nw; i += NTHREADS) {
+            s.moff[i] = b.mass_off[w0 + i] - P0;
+            s.eoff[i] = b.edge_off[w0 + i] - E0;
+            s.uoff[i] = b.muscle_off[w0 + i] - U0;
+        }
+    } else {
+        P0 = w0 * b.M; P1 = w1 * b.M; E0 = w0 * b.K; E1 = w1 * b.K; U0 = w0 * b.A; U1 = w1 * b.A;
+    }
+    const int nP = P1 - P0, nE = E1 - E0, nU = U1 - U0;
+
+    // ================= phase 0: issue every global load of the tile =================
+    stage_in<float4>(s.pos, b.pos + 3 * (size_t)P0, 3 * nP, tid);
+    stage_in<float4>(s.vel, b.vel + 3 * (size_t)P0, 3 * nP, tid);
+    if (!STEP) stage_in<float4>(s.acc, b.acc + 3 * (size_t)P0, 3 * nP, tid);
+    stage_in<float4>(s.m, b.mass + P0, nP, tid);
+    if (STEP && nE > 0)
+        stage_in<uint4>(s.inc, reinterpret_cast<const uint32_t *>(b.inc) + E0, nE, tid);
+
+    // edge records of this lane's first pass -> registers
+    EdgeRec er[EPL];
+    if (STEP) {
+#pragma unroll
+        for (int it = 0; it < EPL; it++) {
+            const int le = tid + it * NTHREADS;
+            if (le < nE) {
+                er[it].ij = b.edge_ij[E0 + le];
+                er[it].rest = b.edge_rest[E0 + le];
+                er[it].k = b.edge_k[E0 + le];
+                er[it].c = b.edge_c[E0 + le];
+                er[it].flag = b.edge_flags ? b.edge_flags[E0 + le] : 0u;
+            }
+        }
+    }
+    // muscles of this lane (first pass) -> registers
+    float mu_x = 0.f, mu_lo = 0.f, mu_hi = 0.f, mu_st = 0.f, mu_a = 0.f;
+    int mu_ua = 0, mu_wl = 0;
+    if (tid < nU) {
+        if (RAGGED) { mu_wl = 0; mu_ua = 0; }
+        else { mu_wl = fdiv(tid, b.A, geo.invA); mu_ua = tid - mu_wl * b.A; }
+        mu_x = b.muscle_x[U0 + tid];
+        if (STEP && action) {
+            mu_lo = b.muscle_lo[U0 + tid];
+            mu_hi = b.muscle_hi[U0 + tid];
+            if (kp.action_mode == 1) mu_st = b.muscle_stride[U0 + tid];
+            if (!RAGGED && mu_ua < action_cols) mu_a = action[(size_t)(w0 + mu_wl) * action_stride + mu_ua];
+        }
+    }
+    // per-walker step counter
+    int wsteps = 0;
+    if (tid < nw) wsteps = b.steps[w0 + tid];
+    if (RAGGED) __syncthreads();   // walker offsets visible before lanes locate their walker
+
+    // this lane's mass (first pass): walker, base, incidence offsets
+    int my_wl = 0, my_lm = 0;
+    if (tid < nP) {
+        if (RAGGED) { my_wl = locate(s.moff, nw, tid); my_lm = s.moff[my_wl]; }
+        else { my_wl = fdiv(tid, b.M, geo.invM); my_lm = my_wl * b.M; }
+    }
+    int io0 = 0, io1 = 0;
+    if (STEP && tid < nP) {
+        const uint16_t *io = b.inc_off + (size_t)(P0 + my_lm) + (size_t)(w0 + my_wl);
+        io0 = io[tid - my_lm];
+        io1 = io[tid - my_lm + 1];
+    }
+
+    // ================= 1. act: Creature.act -> Muscle.act / actdisp -> regulation =================
+    // (gym/optimized_walker.py:27-43,164-172)
+    for (int u = tid; u < nU; u += NTHREADS) {
+        const bool first = (u == tid);
+        float x = first ? mu_x : b.muscle_x[U0 + u];
+        if (STEP && action) {
+            int wl, ua;
+            if (RAGGED) { wl = locate(s.uoff, nw, u); ua = u - s.uoff[wl]; }
+            else if (first) { wl = mu_wl; ua = mu_ua; }
+            else { wl = fdiv(u, b.A, geo.invA); ua = u - wl * b.A; }
+            if (ua < action_cols) {
+                float lo = mu_lo, hi = mu_hi, st = mu_st, a = mu_a;
+                if (!first || RAGGED) {
+                    if (!first) {
+                        lo = b.muscle_lo[U0 + u]; hi = b.muscle_hi[U0 + u];
+                        if (kp.action_mode == 1) st = b.muscle_stride[U0 + u];
+                    }
+                    a = action[(size_t)(w0 + wl) * action_stride + ua];
+                }
+                if (kp.action_mode == 1) x = (a != 0.f) ? x + st : x - st;
+                else x = x + a;
+                if (lo > x) x = lo;     // Python max(x, originx*minl)
+                if (hi < x) x = hi;     // Python min(x, originx*maxl)
+                b.muscle_x[U0 + u] = x;
+            }
+        }
+        s.x[u] = x;
+    }
+    __syncthreads();
+
+    if (STEP) {
+        // ================= 2. edge phase =================
+        // spring (gym/engine.py:78-102) + damping (gym/optimized_walker.py:92-106)
+        for (int pass = 0; pass * EPL * NTHREADS < nE; pass++) {
+#pragma unroll
+            for (int it = 0; it < EPL; it++) {
+                const int le = tid + (pass * EPL + it) * NTHREADS;
+                if (le >= nE) break;
+                EdgeRec e;
+                if (pass == 0) {
+                    e = er[it];
+                } else {
+                    e.ij = b.edge_ij[E0 + le]; e.rest = b.edge_rest[E0 + le];
+                    e.k = b.edge_k[E0 + le]; e.c = b.edge_c[E0 + le];
+                    e.flag = b.edge_flags ? b.edge_flags[E0 + le] : 0u;
+                }
+                if (WG_ABLATE & 1) {
+                    s.t[3 * le] = e.rest; s.t[3 * le + 1] = e.k; s.t[3 * le + 2] = e.c;
+                    s.df[3 * le] = (float)e.ij; s.df[3 * le + 1] = 0.f; s.df[3 * le + 2] = 0.f;
+                    continue;
+                }
+                int lm, ew, Aw, ub;
+                if (RAGGED) {
+                    const int wl = locate(s.eoff, nw, le);
+                    lm = s.moff[wl]; ew = le - s.eoff[wl]; Aw = s.uoff[wl + 1] - s.uoff[wl]; ub = s.uoff[wl];
+                } else {
+                    const int wl = fdiv(le, b.K, geo.invK);
+                    lm = wl * b.M; ew = le - wl * b.K; Aw = b.A; ub = wl * b.A;
+                }
+                const int i = lm + (int)(e.ij & 0xffffu), j = lm + (int)(e.ij >> 16);
+                const float x = (ew < Aw) ? s.x[ub + ew] : e.rest;
+                const float pix = s.pos[3 * i], piy = s.pos[3 * i + 1], piz = s.pos[3 * i + 2];
+                const float pjx = s.pos[3 * j], pjy = s.pos[3 * j + 1], pjz = s.pos[3 * j + 2];
+                const float vix = s.vel[3 * i], viy = s.vel[3 * i + 1], viz = s.vel[3 * i + 2];
+                const float vjx = s.vel[3 * j], vjy = s.vel[3 * j + 1], vjz = s.vel[3 * j + 2];
+                const float cur = np_norm3(pix - pjx, piy - pjy, piz - pjz);   // engine.py:86
+                const float dx = cur - x;                                       // engine.py:96
+                double t0, t1, t2;
+                float d0 = pjx - pix, d1 = pjy - piy, d2 = pjz - piz;
+                double dist = (double)cur;                                      // engine.py:73
+                if (CONFIG_R > dist) dist = CONFIG_R;                           // max(distance, r)
+                const double yc = 1.0 / dist;
+                const bool unit = cur > 0.f;                                    // optimized_walker.py:93
+                if (unit) {
+                    if ((double)cur == dist) {
+                        d0 = fdiv_exact(d0, yc); d1 = fdiv_exact(d1, yc); d2 = fdiv_exact(d2, yc);
+                    } else {
+                        d0 = d0 / cur; d1 = d1 / cur; d2 = d2 / cur;
+                    }
+                }
+                if (kp.spring_mode == 1) {
+                    // G2 element (gym/optimized_walker.py:48-60): float32 force, inverted sign.
+                    const float fs = (-dx) * e.k;
+                    t0 = (double)(fs * d0); t1 = (double)(fs * d1); t2 = (double)(fs * d2);
+                } else {
+                    const float fsz = (dx < 0.f && (e.flag & 1u)) ? 0.f : (-dx) * e.k;   // engine.py:97-100
+                    const float nf = -fsz;                                                // engine.py:75
+                    const float r0 = pjx - pix, r1 = pjy - piy, r2 = pjz - piz;
+                    t0 = ddiv_exact((double)(nf * r0), dist, yc);
+                    t1 = ddiv_exact((double)(nf * r1), dist, yc);
+                    t2 = ddiv_exact((double)(nf * r2), dist, yc);
+                }
+                s.t[3 * le] = t0; s.t[3 * le + 1] = t1; s.t[3 * le + 2] = t2;
+                const float dk = np_dot3(vix - vjx, viy - vjy, viz - vjz, d0, d1, d2);  // :102-103
+                const float dkc = dk * e.c;                                               // :104
+                s.df[3 * le] = dkc * d0; s.df[3 * le + 1] = dkc * d1; s.df[3 * le + 2] = dkc * d2;
+            }
+        }
+        __syncthreads();
+
+        // ================= 3. mass phase: ordered accumulation, env forces, run1 =================
+        const uint16_t *s_inc16 = reinterpret_cast<const uint16_t *>(s.inc);
+        for (int lp = tid; lp < nP; lp += NTHREADS) {
+            const bool first = (lp == tid);
+            int wl, lm, lb;
+            if (first) { wl = my_wl; lm = my_lm; }
+            else if (RAGGED) { wl = locate(s.moff, nw, lp); lm = s.moff[wl]; }
+            else { wl = fdiv(lp, b.M, geo.invM); lm = wl * b.M; }
+            lb = RAGGED ? s.eoff[wl] : wl * b.K;
+            int s0 = io0, s1 = io1;
+            if (!first) {
+                const uint16_t *io = b.inc_off + (size_t)(P0 + lm) + (size_t)(w0 + wl);
+                s0 = io[lp - lm]; s1 = io[lp - lm + 1];
+            }
+            const float mf = s.m[lp];
+            const double md = (double)mf;
+            const double ym = 1.0 / md;      // one IEEE division per mass; every /m below is exact from it
+            float ax = 0.f, ay = 0.f, az = 0.f;
+            for (int r = s0; r < ((WG_ABLATE & 2) ? s0 + 1 : s1); r++) {
+                const int ent = s_inc16[2 * lb + r];
+                const int le = lb + (ent >> 1);
+                const bool end_j = ent & 1;
+                const double t0 = s.t[3 * le], t1 = s.t[3 * le + 1], t2 = s.t[3 * le + 2];
+                const float f0 = s.df[3 * le], f1 = s.df[3 * le + 1], f2 = s.df[3 * le + 2];
+                if (kp.spring_mode == 1) {
+                    const float sg = end_j ? -1.f : 1.f;
+                    ax = ax + fdiv_exact(sg * (float)t0, ym);
+                    ay = ay + fdiv_exact(sg * (float)t1, ym);
+                    az = az + fdiv_exact(sg * (float)t2, ym);
+                } else {
+                    // Point.forced with a float64 force: a = f32(f64(a) + t/m)   (engine.py:67,75)
+                    const double sg = end_j ? -1.0 : 1.0;
+                    ax = (float)((double)ax + ddiv_exact(sg * t0, md, ym));
+                    ay = (float)((double)ay + ddiv_exact(sg * t1, md, ym));
+                    az = (float)((double)az + ddiv_exact(sg * t2, md, ym));
+                }
+                // damping: p1.forced(-damp_force); p2.forced(damp_force)  (optimized_walker.py:105-106)
+                const float sf = end_j ? 1.f : -1.f;
+                ax = ax + fdiv_exact(sf * f0, ym); ay = ay + fdiv_exact(sf * f1, ym); az = az + fdiv_exact(sf * f2, ym);
+            }
+            float vx = s.vel[3 * lp], vy = s.vel[3 * lp + 1], vz = s.vel[3 * lp + 2];
+            float px = s.pos[3 * lp], py = s.pos[3 * lp + 1], pz = s.pos[3 * lp + 2];
+            const float zm = fdiv_exact(0.f, ym);   // the zero components of the env forces, divided by m
+            // gravity [0,-g,0]/m, damp -dampk*v/m  (gym/env.py:32-33, optimized_env.py:148-151)
+            ax = ax + zm; ay = ay + fdiv_exact(kp.neg_g, ym); az = az + zm;
+            ax = ax + fdiv_exact(kp.neg_dampk * vx, ym);
+            ay = ay + fdiv_exact(kp.neg_dampk * vy, ym);
+            az = az + fdiv_exact(kp.neg_dampk * vz, ym);
+            const float deep = py - kp.ground;
+            const bool hit = deep < 0.f;                                     // optimized_env.py:154
+            if (hit) {
+                ax = ax + zm; ay = ay + fdiv_exact(kp.neg_groundk * deep, ym); az = az + zm;
+                ax = ax + zm; ay = ay + fdiv_exact(kp.neg_grounddamp * vy, ym); az = az + zm;
+                const float ff = fabsf(deep) * kp.friction;                   // :168
+                ax = ax + fdiv_exact((-vx) * ff, ym); ay = ay + zm; az = az + fdiv_exact((-vz) * ff, ym);
+            }
+            if (b.contact) b.contact[P0 + lp] = (uint8_t)hit;
+            // Point.run1 (gym/engine.py:174-178)
+            vx = vx + ax * kp.dt; vy = vy + ay * kp.dt; vz = vz + az * kp.dt;
+            px = px + vx * kp.dt; py = py + vy * kp.dt; pz = pz + vz * kp.dt;
+            s.pos[3 * lp] = px; s.pos[3 * lp + 1] = py; s.pos[3 * lp + 2] = pz;
+            s.vel[3 * lp] = vx; s.vel[3 * lp + 1] = vy; s.vel[3 * lp + 2] = vz;
+            s.acc[3 * lp] = ax; s.acc[3 * lp + 1] = ay; s.acc[3 * lp + 2] = az;
+            // reduction terms of the new state: ‖v‖, m*‖v‖^2, f32(m*g)*(y-ground)
+            const float nv = np_norm3(vx, vy, vz);
+            s.nrm[lp] = nv;
+            s.ke[lp] = mf * (nv * nv);   // numpy's float32 ** 2 is libm powf: may differ by 1 ulp
+            s.pe[lp] = (float)(md * kp.g) * (py - kp.ground);
+        }
+    } else {
+        for (int lp = tid; lp < nP; lp += NTHREADS) {
+            const float mf = s.m[lp];
+            const float nv = np_norm3(s.vel[3 * lp], s.vel[3 * lp + 1], s.vel[3 * lp + 2]);
+            s.nrm[lp] = nv;
+            s.ke[lp] = mf * (nv * nv);
+            s.pe[lp] = (float)((double)mf * kp.g) * (s.pos[3 * lp + 1] - kp.ground);
+        }
+    }
+    __syncthreads();
+
+    // ================= write back + per-walker reductions =================
+    if (STEP) {
+        stage_out(b.pos + 3 * (size_t)P0, s.pos, 3 * nP, tid);
+        stage_out(b.vel + 3 * (size_t)P0, s.vel, 3 * nP, tid);
+        stage_out(b.acc + 3 * (size_t)P0, s.acc, 3 * nP, tid);
+    }
+    // 8 lanes per walker, numpy's summation orders (see oracle/walker_oracle.c walker_observe):
+    // r 0-2 sequential sums of pos[:, r] (getstat mid / info centroid), r 3 pairwise sum of y
+    // (np.mean), r 4-6 pairwise sums of |v|, m|v|^2, m*g*(y-ground), r 7 contact count + all-stopped.
+    for (int idx = tid; idx < ((WG_ABLATE & 8) ? 0 : nw * 8); idx += NTHREADS) {
+        const int wl = idx >> 3, r = idx & 7;
+        const int lm = RAGGED ? s.moff[wl] : wl * b.M;
+        const int M = RAGGED ? s.moff[wl + 1] - lm : b.M;
+        float v;
+        if (r == 7) {
+            int hits = 0, all = 1;
+            for (int q = 0; q < M; q++) {
+                hits += (s.pos[3 * (lm + q) + 1] - kp.ground < 0.f);
+                all &= (s.nrm[lm + q] < 0.1f);
+            }
+            v = __int_as_float((hits << 1) | all);
+        } else {
+            const float *src = r < 3 ? s.pos + 3 * lm + r
+                             : r == 3 ? s.pos + 3 * lm + 1
+                             : r == 4 ? s.nrm + lm : r == 5 ? s.ke + lm : s.pe + lm;
+            const int st = r <= 3 ? 3 : 1;
+            if (r < 3) {
+                v = 0.f;
+                for (int q = 0; q < M; q++) v += src[q * st];
+            } else {
+                v = np_pairwise<PWD>(src, M, st);
+            }
+        }
+        s.red[idx] = v;
+    }
+    __syncthreads();
+
+    // ================= per-walker outputs (gym/optimized_env.py:189-248) =================
+    if (tid < nw) {
+        const int wl = tid;
+        const int lm = RAGGED ? s.moff[wl] : wl * b.M;
+        const int M = RAGGED ? s.moff[wl + 1] - lm : b.M;
+        const size_t wg = (size_t)(w0 + wl);
+        const float fM = (float)M;
+        const float *rd = s.red + 8 * wl;
+        const float cy = rd[3] / fM;
+        const int packed = __float_as_int(rd[7]);
+        const int hits = packed >> 1, all = packed & 1;
+        int steps = wsteps;
+        if (STEP) { steps += 1; b.steps[wg] = steps; }
+        if (o.reward) {
+            const float av = rd[4] / fM;
+            const float vpen = (-av) * 0.1f;
+            const float cpen = (float)(-(double)hits * 0.5);
+            o.reward[wg] = (cy + vpen) + cpen;
+        }
+        if (o.done) {
+            int done = steps >= kp.max_steps;
+            if (!done && cy < kp.done_y) done = 1;
+            if (!done && steps > 100) done = all;
+            o.done[wg] = (uint8_t)done;
+        }
+        if (o.centroid) {
+            o.centroid[3 * wg] = rd[0] / fM; o.centroid[3 * wg + 1] = rd[1] / fM; o.centroid[3 * wg + 2] = rd[2] / fM;
+        }
+        if (o.energy) o.energy[wg] = 0.5f * rd[5] + rd[6];
+    }
+
+    // ================= observation rows: Creature.getstat (gym/optimized_walker.py:129-162) =================
+    if (o.obs && !(WG_ABLATE & 16)) {
+        constexpr int d = IN3D ? 3 : 2, per = 3 * d;
+        const int stride = o.obs_stride;
+        float *ob = o.obs + (size_t)w0 * stride;
+        // uniform batches assemble the rows in LDS (aliasing the dead spring-term region) and stream
+        // them out as one contiguous 16-B-store block; ragged batches write rows directly.
+        float *tile = RAGGED ? nullptr : reinterpret_cast<float *>(s.t);
+        const int nmid = kp.conmid ? 3 : 0;
+        // per-mass block of 3*d values: (pos - mid)*pk, v*vk, old_a*ak
+        for (int lp = tid; lp < nP; lp += NTHREADS) {
+            int wl, lm;
+            if (lp == tid) { wl = my_wl; lm = my_lm; }
+            else if (RAGGED) { wl = locate(s.moff, nw, lp); lm = s.moff[wl]; }
+            else { wl = fdiv(lp, b.M, geo.invM); lm = wl * b.M; }
+            const int M = RAGGED ? s.moff[wl + 1] - lm : b.M;
+            const float fM = (float)M;
+            float *row = (RAGGED ? ob : tile) + (size_t)wl * stride + per * (lp - lm);
+#pragma unroll
+            for (int c = 0; c < d; c++) {
+                const float pv = s.pos[3 * lp + c];
+                row[c] = kp.midform ? (pv - s.red[8 * wl + c] / fM) * kp.pk : pv * kp.pk;
+                row[d + c] = s.vel[3 * lp + c] * kp.vk;
+                row[2 * d + c] = s.acc[3 * lp + c] * kp.ak;
+            }
+        }
+        // muscle rest lengths x*mk
+        for (int u = tid; u < nU; u += NTHREADS) {
+            int wl, ua, M;
+            if (RAGGED) { wl = locate(s.uoff, nw, u); ua = u - s.uoff[wl]; M = s.moff[wl + 1] - s.moff[wl]; }
+            else { wl = fdiv(u, b.A, geo.invA); ua = u - wl * b.A; M = b.M; }
+            (RAGGED ? ob : tile)[(size_t)wl * stride + per * M + nmid + ua] = s.x[u] * kp.mk;
+        }
+        // conmid columns and zero padding of short (ragged) rows
+        for (int wl = tid; wl < nw; wl += NTHREADS) {
+            const int lm = RAGGED ? s.moff[wl] : wl * b.M;
+            const int M = RAGGED ? s.moff[wl + 1] - lm : b.M;
+            const int A = RAGGED ? s.uoff[wl + 1] - s.uoff[wl] : b.A;
+            float *row = (RAGGED ? ob : tile) + (size_t)wl * stride;
+            if (nmid)
+                for (int c = 0; c < 3; c++) row[per * M + c] = kp.midform ? s.red[8 * wl + c] / (float)M : 0.f;
+            for (int r = per * M + nmid + A; r < stride; r++) row[r] = 0.f;
+        }
+        if (!RAGGED) {
+            __syncthreads();
+            stage_out(ob, tile, nw * stride, tid);
+        }
+    }
+}
+
+// reset: v += noise (x, y, z if in3d), steps = 0 (PhysicsEnv.reset, gym/optimized_env.py:53-68)
+__global__ void walker_reset_kernel(wg_batch b, const float *__restrict__ noise, const uint8_t *__restrict__ mask,
+                                    int in3d) {
+    const int P = b.ragged ? b.mass_off[b.N] : b.N * b.M;
+    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < P; q += gridDim.x * blockDim.x) {
+        int w;
+        if (b.ragged) {
+            int lo = 0, hi = b.N - 1;
+            while (lo < hi) { const int mid = (lo + hi + 1) >> 1; if (b.mass_off[mid] <= q) lo = mid; else hi = mid - 1; }
+            w = lo;
+        } else {
+            w = q / b.M;
+        }
+        if (mask && !mask[w]) continue;
+        if (noise) {
+            b.vel[3 * q] = b.vel[3 * q] + noise[3 * q];
+            b.vel[3 * q + 1] = b.vel[3 * q + 1] + noise[3 * q + 1];
+            if (in3d) b.vel[3 * q + 2] = b.vel[3 * q + 2] + noise[3 * q + 2];
+        }
+    }
+    for (int w = blockIdx.x * blockDim.x + threadIdx.x; w < b.N; w += gridDim.x * blockDim.x)
+        if (!mask || mask[w]) b.steps[w] = 0;
+}
+
+// ------------------------------------------------------------------ host side
+KParams make_kparams(const wg_params &p) {
+    KParams k;
+    k.neg_g = (float)(-p.g);
+    k.neg_dampk = (float)(-p.dampk);
+    k.ground = (float)p.ground;
+    k.neg_groundk = (float)(-p.groundk);
+    k.neg_grounddamp = (float)(-p.grounddamp);
+    k.friction = (float)p.friction;
+    k.dt = (float)p.dt;
+    k.pk = (float)p.pk; k.vk = (float)p.vk; k.ak = (float)p.ak; k.mk = (float)p.mk;
+    k.done_y = (float)(p.ground - 50.0);
+    k.g = p.g;
+    k.max_steps = p.max_steps; k.midform = p.midform; k.conmid = p.conmid;
+    k.spring_mode = p.spring_mode; k.action_mode = p.action_mode;
+    return k;
+}
+
+constexpr int RAG_P = 256, RAG_E = 512, RAG_U = 256, RAG_W = 64;
+constexpr int LDS_LIMIT = 160 * 1024;
+
+int validate(const wg_batch *b) {
+    if (!b) return fail(WG_EINVAL, "null batch");
+    if (b->N < 0 || b->M < 1 || b->K < 0 || b->A < 0 || b->A > b->K)
+        return fail(WG_EINVAL, "bad sizes N=%d M=%d K=%d A=%d", b->N, b->M, b->K, b->A);
+    if (2 * b->K > 65535) return fail(WG_ERANGE, "K=%d exceeds the u16 incidence encoding", b->K);
+    if (b->M > WG_MAX_M) return fail(WG_ERANGE, "M=%d > %d masses per walker", b->M, WG_MAX_M);
+    if (!b->pos || !b->vel || !b->acc || !b->mass || !b->steps || !b->muscle_x)
+        return fail(WG_EINVAL, "missing state pointer");
+    if (b->K > 0 && (!b->edge_ij || !b->edge_rest || !b->edge_k || !b->edge_c || !b->inc || !b->inc_off))
+        return fail(WG_EINVAL, "missing edge pointer");
+    if (!b->inc_off) return fail(WG_EINVAL, "missing inc_off");
+    if (b->ragged && (!b->mass_off || !b->edge_off || !b->muscle_off))
+        return fail(WG_EINVAL, "ragged batch without offsets");
+    return 0;
+}
+
+Geo uniform_geo(const wg_batch *b, int obs_stride) {
+    Geo g;
+    g.threads = NTHREADS;
+    // walkers per workgroup: fill the 256 mass lanes, keep edges within EPL registers per lane,
+    // and make sure the grid has >= 512 workgroups when the batch allows it.
+    int W = std::max(1, NTHREADS / b->M);
+    if (b->K > 0) W = std::max(1, std::min(W, EPL * NTHREADS / std::max(1, b->K)));
+    while (W > 1 && (b->N + W - 1) / W < 512) W = std::max(1, W / 2);
+    g.W = W;
+    for (;;) {
+        g.Pcap = g.W * b->M; g.Ecap = g.W * b->K; g.Ucap = g.W * b->A;
+        g.tbytes = std::max(g.Ecap * 3 * 8, g.W * std::max(0, obs_stride) * 4);
+        g.lds = carve_bytes(g);
+        if (g.lds <= 64 * 1024 || g.W == 1) break;
+        g.W = std::max(1, g.W / 2);
+    }
+    g.invM = 1.f / (float)b->M;
+    g.invK = 1.f / (float)std::max(1, b->K);
+    g.invA = 1.f / (float)std::max(1, b->A);
+    return g;
+}
+
+Geo ragged_geo(const wg_batch *b) {
+    Geo g;
+    g.threads = NTHREADS;
+    g.W = RAG_W;
+    g.Pcap = std::max(RAG_P, b->M);
+    g.Ecap = std::max(RAG_E, b->K);
+    g.Ucap = std::max(RAG_U, b->A);
+    g.tbytes = g.Ecap * 3 * 8;
+    g.lds = carve_bytes(g);
+    g.invM = g.invK = g.invA = 0.f;
+    return g;
+}
+
+template <bool STEP, bool RAGGED, bool IN3D, int PWD>
+int launch(const wg_batch *b, const KParams &kp, const float *action, int cols, int astride,
+           const wg_outputs &o, const int32_t *plan, int blocks, const Geo &g, hipStream_t stream) {
+    if (g.lds > LDS_LIMIT) return fail(WG_ERANGE, "workgroup needs %d B of LDS (> 160 KiB)", g.lds);
+    hipLaunchKernelGGL((walker_step_kernel<STEP, RAGGED, IN3D, PWD>), dim3(blocks), dim3(g.threads), g.lds, stream,
+                       *b, kp, action, cols, astride, o, plan, g);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(WG_EHIP, "launch failed: %s", hipGetErrorString(e));
+    return 0;
+}
+
+template <bool STEP, int PWD>
+int dispatch2(const wg_batch *b, const KParams &kp, bool in3d, const float *a, int cols, int astride,
+              const wg_outputs &o, const int32_t *plan, int blocks, const Geo &g, hipStream_t st) {
+    if (b->ragged) {
+        return in3d ? launch<STEP, true, true, PWD>(b, kp, a, cols, astride, o, plan, blocks, g, st)
+                    : launch<STEP, true, false, PWD>(b, kp, a, cols, astride, o, plan, blocks, g, st);
+    }
+    return in3d ? launch<STEP, false, true, PWD>(b, kp, a, cols, astride, o, plan, blocks, g, st)
+                : launch<STEP, false, false, PWD>(b, kp, a, cols, astride, o, plan, blocks, g, st);
+}
+template <bool STEP>
+int dispatch(const wg_batch *b, const KParams &kp, bool in3d, const float *a, int cols, int astride,
+             const wg_outputs &o, const int32_t *plan, int blocks, const Geo &g, hipStream_t st) {
+    return b->M <= 128 ? dispatch2<STEP, 0>(b, kp, in3d, a, cols, astride, o, plan, blocks, g, st)
+                       : dispatch2<STEP, 3>(b, kp, in3d, a, cols, astride, o, plan, blocks, g, st);
+}
+
+int run(const wg_batch *b, const wg_params *p, const float *action, int32_t cols, int32_t astride,
+        int64_t astep, const wg_outputs *o, int32_t n_steps, const int32_t *plan, int32_t plan_blocks,
+        hipStream_t stream, bool step) {
+    int rc = validate(b);
+    if (rc) return rc;
+    if (!p) return fail(WG_EINVAL, "null params");
+    if (b->N == 0 || n_steps <= 0) return 0;
+    if (action && (cols < 0 || astride < cols)) return fail(WG_EINVAL, "bad action stride");
+    if (action && p->action_mode == 1 && !b->muscle_stride) return fail(WG_EINVAL, "discrete actions need muscle_stride");
+    if (action && (!b->muscle_lo || !b->muscle_hi)) return fail(WG_EINVAL, "actions need muscle_lo/hi");
+    if (b->ragged && (!plan || plan_blocks <= 0)) return fail(WG_EINVAL, "ragged batch needs a plan");
+    wg_outputs out = o ? *o : wg_outputs{};
+    if (out.obs && out.obs_stride <= 0) return fail(WG_EINVAL, "obs_stride must be > 0");
+    const KParams kp = make_kparams(*p);
+    const Geo g = b->ragged ? ragged_geo(b) : uniform_geo(b, out.obs ? out.obs_stride : 0);
+    if (g.W > NTHREADS) return fail(WG_ERANGE, "more than %d walkers per workgroup", NTHREADS);
+    const int blocks = b->ragged ? plan_blocks : (b->N + g.W - 1) / g.W;
+    for (int s = 0; s < n_steps; s++) {
+        wg_outputs os = out;
+        if (os.obs) os.obs += s * os.obs_step;
+        if (os.reward) os.reward += s * os.out_step;
+        if (os.done) os.done += s * os.out_step;
+        if (os.energy) os.energy += s * os.out_step;
+        if (os.centroid) os.centroid += 3 * s * os.out_step;
+        const float *a = action ? action + s * astep : nullptr;
+        rc = step ? dispatch<true>(b, kp, p->in3d != 0, a, cols, astride, os, plan, blocks, g, stream)
+                  : dispatch<false>(b, kp, p->in3d != 0, nullptr, 0, 0, os, plan, blocks, g, stream);
+        if (rc) return rc;
+    }
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int wg_abi_version(void) { return WG_ABI_VERSION; }
+const char *wg_last_error(void) { return g_err; }
+
+int wg_step(const wg_batch *b, const wg_params *p, const float *action, int32_t action_cols,
+            int32_t action_stride, int64_t action_step, const wg_outputs *o, int32_t n_steps,
+            const int32_t *plan, int32_t plan_blocks, hipStream_t stream) {
+    return run(b, p, action, action_cols, action_stride, action_step, o, n_steps, plan, plan_blocks, stream, true);
+}
+
+int wg_observe(const wg_batch *b, const wg_params *p, const wg_outputs *o, const int32_t *plan,
+               int32_t plan_blocks, hipStream_t stream) {
+    if (!o) return fail(WG_EINVAL, "null outputs");
+    return run(b, p, nullptr, 0, 0, 0, o, 1, plan, plan_blocks, stream, false);
+}
+
+int wg_reset(const wg_batch *b, const wg_params *p, const float *noise, const uint8_t *mask, hipStream_t stream) {
+    int rc = validate(b);
+    if (rc) return rc;
+    if (!p) return fail(WG_EINVAL, "null params");
+    if (b->N == 0) return 0;
+    const long P = b->ragged ? -1 : (long)b->N * b->M;
+    const int blocks = P > 0 ? (int)std::min<long>((P + 255) / 256, 4096) : 1024;
+    hipLaunchKernelGGL(walker_reset_kernel, dim3(blocks), dim3(256), 0, stream, *b, noise, mask, p->in3d);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(WG_EHIP, "reset launch failed: %s", hipGetErrorString(e));
+    return 0;
+}
+
+int wg_plan_ragged(const int32_t *mass_off, const int32_t *edge_off, const int32_t *muscle_off,
+                   int32_t N, int32_t *plan, int32_t max_blocks) {
+    if (!mass_off || !edge_off || !muscle_off || !plan || N < 0 || max_blocks < 1)
+        return fail(WG_EINVAL, "bad plan args");
+    int blocks = 0;
+    plan[0] = 0;
+    int w = 0;
+    while (w < N) {
+        int P = 0, E = 0, U = 0, n = 0;
+        while (w < N) {
+            const int m = mass_off[w + 1] - mass_off[w], k = edge_off[w + 1] - edge_off[w],
+                      a = muscle_off[w + 1] - muscle_off[w];
+            if (n > 0 && (P + m > RAG_P || E + k > RAG_E || U + a > RAG_U || n + 1 > RAG_W)) break;
+            P += m; E += k; U += a; n++; w++;
+        }
+        if (blocks + 1 > max_blocks) return fail(WG_ERANGE, "plan needs more than %d blocks", max_blocks);
+        plan[++blocks] = w;
+    }
+    return blocks;
+}
+
+int wg_launch_geometry(const wg_batch *b, wg_launch_info *info) {
+    int rc = validate(b);
+    if (rc) return rc;
+    if (!info) return fail(WG_EINVAL, "null info");
+    const Geo g = b->ragged ? ragged_geo(b) : uniform_geo(b, 0);
+    info->threads = g.threads;
+    info->walkers_per_block = g.W;
+    info->blocks = b->ragged ? -1 : (b->N + g.W - 1) / g.W;
+    info->lds_bytes = g.lds;
+    return 0;
+}
+
+}  // extern "C"

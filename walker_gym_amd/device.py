@@ -1,0 +1,114 @@
+"""Device-resident walker batch: the HostLayout uploaded to PyTorch-ROCm tensors in HBM, plus the
+ctypes structs handed to libwalker_hip.so.  PyTorch is plumbing here (allocation, streams,
+torch.distributed); all per-step compute is the HIP kernel."""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import _lib
+from .layout import HostLayout
+
+_TORCH = {np.dtype(np.float32): torch.float32, np.dtype(np.int32): torch.int32,
+          np.dtype(np.uint8): torch.uint8}
+
+
+def _to_dev(a: np.ndarray, device) -> torch.Tensor:
+    a = np.ascontiguousarray(a)
+    if a.dtype == np.uint16:
+        t = torch.from_numpy(a.view(np.int16))
+    elif a.dtype == np.uint32:
+        t = torch.from_numpy(a.view(np.int32))
+    else:
+        t = torch.from_numpy(a)
+    return t.to(device, non_blocking=False).contiguous()
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+class DeviceBatch:
+    """All walker arrays as device tensors (owned here, borrowed by the kernel per launch)."""
+
+    STATE = ("pos", "vel", "acc", "muscle_x", "steps")
+
+    def __init__(self, host: HostLayout, device: torch.device, contact: bool = True):
+        if device.type != "cuda":
+            raise ValueError("DeviceBatch needs a ROCm device (torch 'cuda' device); there is no CPU path")
+        self.host = host
+        self.device = device
+        self.N, self.M, self.K, self.A, self.ragged = host.N, host.M, host.K, host.A, host.ragged
+        self.P, self.E, self.U = host.P, host.E, host.U
+        dv = device
+        self.mass_off = _to_dev(host.mass_off, dv)
+        self.edge_off = _to_dev(host.edge_off, dv)
+        self.muscle_off = _to_dev(host.muscle_off, dv)
+        self.pos = _to_dev(host.pos, dv)
+        self.vel = _to_dev(host.vel, dv)
+        self.acc = _to_dev(host.acc, dv)
+        self.mass = _to_dev(host.mass, dv)
+        self.edge_ij = _to_dev(host.edge_ij, dv)
+        self.edge_rest = _to_dev(host.edge_rest, dv)
+        self.edge_k = _to_dev(host.edge_k, dv)
+        self.edge_c = _to_dev(host.edge_c, dv)
+        self.edge_flags = _to_dev(host.edge_flags, dv) if host.edge_flags.any() else None
+        self.inc = _to_dev(host.inc, dv) if host.E else None
+        self.inc_off = _to_dev(host.inc_off, dv)
+        self.muscle_x = _to_dev(host.muscle_x, dv)
+        self.muscle_lo = _to_dev(host.muscle_lo, dv)
+        self.muscle_hi = _to_dev(host.muscle_hi, dv)
+        self.muscle_stride = _to_dev(host.muscle_stride, dv)
+        self.steps = _to_dev(host.steps, dv)
+        self.contact = torch.zeros(self.P, dtype=torch.uint8, device=dv) if contact else None
+        # placeholders so that zero-size arrays still have a valid device pointer
+        self._dummy = torch.zeros(16, dtype=torch.float32, device=dv)
+        self.plan = None
+        self.plan_blocks = 0
+        if self.ragged:
+            L = _lib.load()
+            plan = np.zeros(self.N + 1, np.int32)
+            nb = _lib.check(L.wg_plan_ragged(host.mass_off.ctypes.data_as(C.c_void_p),
+                                             host.edge_off.ctypes.data_as(C.c_void_p),
+                                             host.muscle_off.ctypes.data_as(C.c_void_p), self.N,
+                                             plan.ctypes.data_as(C.c_void_p), self.N + 1), "wg_plan_ragged")
+            self.plan = _to_dev(plan[:nb + 1], dv)
+            self.plan_blocks = nb
+        self.struct = self._make_struct()
+
+    def _p(self, t):
+        if t is None:
+            return None
+        if t.numel() == 0:
+            return C.c_void_p(self._dummy.data_ptr())
+        return C.c_void_p(t.data_ptr())
+
+    def _make_struct(self) -> _lib.WgBatch:
+        r = self.ragged
+        return _lib.WgBatch(
+            N=self.N, M=self.M, K=self.K, A=self.A, ragged=int(r),
+            mass_off=self._p(self.mass_off) if r else None, edge_off=self._p(self.edge_off) if r else None,
+            muscle_off=self._p(self.muscle_off) if r else None,
+            pos=self._p(self.pos), vel=self._p(self.vel), acc=self._p(self.acc), mass=self._p(self.mass),
+            edge_ij=self._p(self.edge_ij), edge_rest=self._p(self.edge_rest), edge_k=self._p(self.edge_k),
+            edge_c=self._p(self.edge_c), edge_flags=self._p(self.edge_flags),
+            inc=self._p(self.inc) if self.inc is not None else None, inc_off=self._p(self.inc_off),
+            muscle_x=self._p(self.muscle_x), muscle_lo=self._p(self.muscle_lo), muscle_hi=self._p(self.muscle_hi),
+            muscle_stride=self._p(self.muscle_stride), steps=self._p(self.steps), contact=self._p(self.contact))
+
+    def launch_geometry(self) -> dict:
+        info = _lib.WgLaunchInfo()
+        _lib.check(_lib.load().wg_launch_geometry(C.byref(self.struct), C.byref(info)), "wg_launch_geometry")
+        blocks = self.plan_blocks if self.ragged else info.blocks
+        return dict(threads=info.threads, walkers_per_block=info.walkers_per_block, blocks=blocks,
+                    lds_bytes=info.lds_bytes)
+
+    def state_dict(self) -> dict:
+        return {k: getattr(self, k).clone() for k in self.STATE}
+
+    def load_state_dict(self, sd: dict) -> None:
+        for k in self.STATE:
+            getattr(self, k).copy_(sd[k])

@@ -1,0 +1,103 @@
+"""Point / Config: the reference's engine objects as host-side descriptions of walker masses.
+
+Mirrors gym/engine.py:7-59 (Config, to_data, Point.__init__/params) so reference-style builder code
+(``Point(m, pos, v)``, ``Muscle(p1, p2)``, ``Creature(...)``) works unchanged.  A Point here holds the
+INITIAL state; once its creature is packed into an env (walker_gym_amd.optimized_env.PhysicsEnv /
+walker_gym_amd.env.Environment), ``pos``, ``v``, ``a`` and ``old_a`` read the live device state.
+The per-point physics methods of the reference (forced, anti_forced, resilience, run1) are what
+the HIP kernel executes batched; they are not methods here.
+"""
+from __future__ import annotations
+
+from typing import Tuple, Union
+
+import numpy as np
+
+
+class Config:
+    """gym/engine.py:7-12."""
+    precision = np.float32
+    r = 16e-36
+    e = 16e-20
+    k = 8.99e9
+    g = 9.8
+
+
+def to_data(data) -> np.ndarray:
+    """gym/engine.py:14-21."""
+    if isinstance(data, (tuple, list)):
+        return np.array(data, dtype=Config.precision)
+    if isinstance(data, np.ndarray):
+        return data.astype(Config.precision)
+    raise TypeError(f"Data must be a numpy array, tuple, list (not {type(data).__name__})")
+
+
+class Point:
+    """A point mass (gym/engine.py:24-59).  ``_env``/``_index`` are set when the owning creature is
+    packed into an env; attribute reads then come from the device tensors."""
+
+    def __init__(self, m: float, pos, v, r: float = None,
+                 color: Union[str, Tuple[int, int, int]] = "black", e: float = Config.e):
+        self.m = m
+        self._pos = to_data(pos)
+        self._v = to_data(v)
+        self._a = np.zeros_like(self._v, dtype=Config.precision)
+        self._old_a = self._a.copy()
+        self.r = m ** 0.3 if r is None else r
+        self.color = color
+        self.e = e
+        self._env = None
+        self._index = -1
+
+    # live views -------------------------------------------------------------------------------
+    def _live(self, name):
+        if self._env is None:
+            return getattr(self, "_" + name)
+        return self._env._point_state(self._index, name)
+
+    @property
+    def pos(self):
+        return self._live("pos")
+
+    @pos.setter
+    def pos(self, value):
+        if self._env is None:
+            self._pos = to_data(value)
+        else:
+            self._env._set_point_state(self._index, "pos", value)
+
+    @property
+    def v(self):
+        return self._live("v")
+
+    @v.setter
+    def v(self, value):
+        if self._env is None:
+            self._v = to_data(value)
+        else:
+            self._env._set_point_state(self._index, "v", value)
+
+    @property
+    def old_a(self):
+        return self._live("old_a")
+
+    @property
+    def a(self):
+        # between steps the reference's `a` is zero (run1 zeroes it, gym/engine.py:178)
+        return np.zeros(3, dtype=Config.precision) if self._env is not None else self._a
+
+    def __repr__(self):
+        return f"Point(m={self.m}, pos={self.pos}, v={self.v}, a={self.old_a})"
+
+    def params(self):
+        return {"m": self.m, "v": self.v.tolist(), "a": self.a.tolist(), "pos": self.pos.tolist(),
+                "r": self.r, "e": self.e, "color": self.color, "old_a": self.old_a.tolist()}
+
+
+class DingPoint(Point):
+    """Pinned point (gym/optimized_engine.py:404-426).  Recognised by the packer, which rejects it:
+    pinned nodes are a SURVEY §8(f) 'next' item not implemented by the kernel yet."""
+
+    def __init__(self, m, p, v=None, r=None, color="black"):
+        super().__init__(m, p, [0, 0, 0] if v is None else v, r, color)
+        self.original_pos = np.array(self._pos, copy=True)

@@ -1,0 +1,182 @@
+"""Walker topology packer and HBM layout.
+
+The reference keeps one Python object per mass (gym/engine.py:24-59) and per edge
+(gym/optimized_walker.py:7-106).  Here a batch of walkers is flat structure-of-arrays in HBM,
+ordered by walker so that any contiguous walker range is a contiguous byte range of every array:
+
+  per mass   pos, vel, acc (old_a)  f32[P,3];  mass f32[P];  contact u8[P]
+  per edge   edge_ij u32[E] (i | j<<16, walker-local);  rest, k, c f32[E];  flags u8[E]
+  per walker-edge-end   inc u16[2E] = (edge<<1 | end) sorted by (mass, edge, end);
+             inc_off u16[P+N] (M_w+1 offsets per walker) — the deterministic accumulation order
+  per muscle muscle_x, lo = f32(originx*minl), hi = f32(originx*maxl), stride  f32[U]
+  per walker steps i32[N]
+Muscles are the first A_w edges of each walker (Creature.run order, gym/optimized_walker.py:124-127).
+Uniform batches (one M/K/A) carry no offsets; ragged ones carry CSR mass_off/edge_off/muscle_off.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, Optional
+
+import numpy as np
+
+f32 = np.float32
+SPEC_KEYS = ("m", "pos", "vel", "mass_off", "ei", "ej", "rest", "k", "c", "flags", "edge_off", "n_muscles",
+             "minl", "maxl", "stride")
+
+
+@dataclass
+class HostLayout:
+    """Packed host arrays, ready to upload.  All arrays are C-contiguous numpy."""
+    N: int
+    M: int            # uniform: masses per walker; ragged: max
+    K: int
+    A: int
+    ragged: bool
+    mass_off: np.ndarray
+    edge_off: np.ndarray
+    muscle_off: np.ndarray
+    pos: np.ndarray
+    vel: np.ndarray
+    acc: np.ndarray
+    mass: np.ndarray
+    edge_ij: np.ndarray
+    edge_rest: np.ndarray
+    edge_k: np.ndarray
+    edge_c: np.ndarray
+    edge_flags: np.ndarray
+    inc: np.ndarray
+    inc_off: np.ndarray
+    muscle_x: np.ndarray
+    muscle_lo: np.ndarray
+    muscle_hi: np.ndarray
+    muscle_stride: np.ndarray
+    steps: np.ndarray
+    extra: Dict[str, np.ndarray] = field(default_factory=dict)
+
+    @property
+    def P(self) -> int:
+        return int(self.mass_off[-1])
+
+    @property
+    def E(self) -> int:
+        return int(self.edge_off[-1])
+
+    @property
+    def U(self) -> int:
+        return int(self.muscle_off[-1])
+
+    def obs_len(self, in3d: bool, conmid: bool) -> np.ndarray:
+        d = 3 if in3d else 2
+        return (3 * d * np.diff(self.mass_off) + (3 if conmid else 0) + np.diff(self.muscle_off)).astype(np.int32)
+
+
+def incidence(ei: np.ndarray, ej: np.ndarray, mass_off: np.ndarray, edge_off: np.ndarray):
+    """Per-walker incidence lists in reference accumulation order.
+
+    For mass q of walker w the list holds (e<<1 | end) for every edge e of w with ei[e]==q (end 0) or
+    ej[e]==q (end 1), sorted by e then end — the order in which gym/optimized_walker.py:124-127 +
+    gym/engine.py:101-102 add spring/damping terms to q's acceleration.
+    Returns inc u16[2E] (walker w's list at 2*edge_off[w]) and inc_off u16[P+N]
+    (walker w's M_w+1 offsets at mass_off[w]+w, walker-local)."""
+    N = len(mass_off) - 1
+    Ks = np.diff(edge_off).astype(np.int64)
+    Ms = np.diff(mass_off).astype(np.int64)
+    E = int(edge_off[-1])
+    if E and (Ks.max() * 2 > 65535):
+        raise ValueError("a walker with more than 32767 edges does not fit the u16 incidence encoding")
+    wid = np.repeat(np.arange(N, dtype=np.int64), Ks)
+    local_e = np.arange(E, dtype=np.int64) - np.repeat(edge_off[:-1].astype(np.int64), Ks)
+    # two entries per edge: (mass, edge, end)
+    mass = np.stack([ei.astype(np.int64), ej.astype(np.int64)], 1).reshape(-1)
+    end = np.tile(np.array([0, 1], np.int64), E)
+    e2 = np.repeat(local_e, 2)
+    w2 = np.repeat(wid, 2)
+    if E and (mass.min() < 0 or np.any(mass >= np.repeat(Ms, 2 * Ks))):
+        raise ValueError("edge endpoint out of range of its walker")
+    maxk = int(Ks.max()) if N else 0
+    key = ((w2 * (int(Ms.max()) + 1 if N else 1) + mass) * (2 * maxk + 2) + 2 * e2 + end)
+    order = np.argsort(key, kind="stable")
+    inc = ((e2[order] << 1) | end[order]).astype(np.uint16)
+    # counts per (walker, mass) -> offsets
+    counts = np.zeros(int(mass_off[-1]), np.int64)
+    np.add.at(counts, np.repeat(mass_off[:-1].astype(np.int64), 2 * Ks) + mass, 1)
+    inc_off = np.zeros(int(mass_off[-1]) + N, np.uint16)
+    for_w = np.repeat(np.arange(N, dtype=np.int64), Ms)
+    csum = np.cumsum(counts)
+    start_w = np.concatenate([[0], csum])[mass_off[:-1].astype(np.int64)]   # global start of walker
+    excl = np.concatenate([[0], csum[:-1]]) - start_w[for_w]                 # walker-local start of mass
+    q_local = np.arange(int(mass_off[-1]), dtype=np.int64) - mass_off[:-1].astype(np.int64)[for_w]
+    pos_in = mass_off[:-1].astype(np.int64)[for_w] + for_w + q_local
+    inc_off[pos_in] = excl.astype(np.uint16)
+    inc_off[(mass_off[1:].astype(np.int64) + np.arange(N))] = (2 * Ks).astype(np.uint16)
+    return inc, inc_off
+
+
+def pack(spec: Dict[str, np.ndarray], mx: Optional[np.ndarray] = None, steps: Optional[np.ndarray] = None) -> HostLayout:
+    """Pack a flat CSR spec (see walker_gym_amd.synthetic) into the HBM layout."""
+    s = {k: np.asarray(spec[k]) for k in SPEC_KEYS}
+    if mx is None:
+        mx = spec.get("mx")
+    mass_off = np.ascontiguousarray(s["mass_off"], np.int32)
+    edge_off = np.ascontiguousarray(s["edge_off"], np.int32)
+    n_mus = np.ascontiguousarray(s["n_muscles"], np.int32)
+    N = len(mass_off) - 1
+    muscle_off = np.concatenate([[0], np.cumsum(n_mus)]).astype(np.int32)
+    Ms, Ks = np.diff(mass_off), np.diff(edge_off)
+    if N == 0:
+        raise ValueError("empty batch")
+    if np.any(Ms < 1):
+        raise ValueError("every walker needs at least one mass")
+    if np.any(n_mus > Ks):
+        raise ValueError("a walker has more muscles than edges (muscles are the first edges)")
+    if Ms.max() > 1024:
+        raise ValueError("walkers with more than 1024 masses are not supported (WG_MAX_M)")
+    ragged = not (np.all(Ms == Ms[0]) and np.all(Ks == Ks[0]) and np.all(n_mus == n_mus[0]))
+    ei = np.ascontiguousarray(s["ei"], np.int64)
+    ej = np.ascontiguousarray(s["ej"], np.int64)
+    edge_ij = (ei.astype(np.uint32) | (ej.astype(np.uint32) << np.uint32(16))).astype(np.uint32)
+    inc, inc_off = incidence(ei, ej, mass_off, edge_off)
+    rest = np.ascontiguousarray(s["rest"], f32)
+    # muscle u of walker w is edge edge_off[w] + (u - muscle_off[w]); originx = its rest
+    uw = np.repeat(np.arange(N), n_mus)
+    medge = edge_off[:-1][uw] + (np.arange(int(muscle_off[-1])) - muscle_off[:-1][uw])
+    x0 = rest[medge]
+    minl = np.ascontiguousarray(s["minl"], f32)
+    maxl = np.ascontiguousarray(s["maxl"], f32)
+    # Muscle.regulation computes originx*minl / originx*maxl in float32 each call (optimized_walker.py:29-30)
+    lo = (x0 * minl).astype(f32)
+    hi = (x0 * maxl).astype(f32)
+    pos = np.ascontiguousarray(s["pos"], f32).reshape(-1, 3)
+    acc = spec.get("acc")
+    return HostLayout(
+        N=N, M=int(Ms.max()), K=int(Ks.max()), A=int(n_mus.max()), ragged=bool(ragged),
+        mass_off=mass_off, edge_off=edge_off, muscle_off=muscle_off,
+        pos=pos.copy(), vel=np.ascontiguousarray(s["vel"], f32).reshape(-1, 3).copy(),
+        acc=(np.zeros_like(pos) if acc is None else np.ascontiguousarray(acc, f32).reshape(-1, 3).copy()),
+        mass=np.ascontiguousarray(s["m"], f32), edge_ij=edge_ij, edge_rest=rest,
+        edge_k=np.ascontiguousarray(s["k"], f32), edge_c=np.ascontiguousarray(s["c"], f32),
+        edge_flags=np.ascontiguousarray(s["flags"], np.uint8), inc=inc, inc_off=inc_off,
+        muscle_x=(x0.copy() if mx is None else np.ascontiguousarray(mx, f32).copy()),
+        muscle_lo=lo, muscle_hi=hi, muscle_stride=np.ascontiguousarray(s["stride"], f32),
+        steps=(np.zeros(N, np.int32) if steps is None else np.ascontiguousarray(steps, np.int32).copy()),
+    )
+
+
+def algorithmic_bytes_per_walker_step(M: int, K: int, A: int, obs_floats: int) -> int:
+    """B = 64M + 16K + 20A + 8 (+ 4 per materialised obs float)."""
+    return 64 * M + 16 * K + 20 * A + 8 + 4 * obs_floats
+
+
+def layout_bytes_per_walker_step(M: int, K: int, A: int, obs_floats: int, info: bool = True,
+                                 contact: bool = True) -> int:
+    """Bytes THIS layout moves per walker-step (the survey's B plus what the layout adds):
+    incidence lists u16[2K] + offsets u16[M+1], centroid/energy (16 B) and contact (M B); the muscle
+    edges' unused rest entries are not read (-4A)."""
+    b = algorithmic_bytes_per_walker_step(M, K, A, obs_floats)
+    b += 2 * 2 * K + 2 * (M + 1) - 4 * A
+    if info:
+        b += 16
+    if contact:
+        b += M
+    return b

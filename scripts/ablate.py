@@ -9,8 +9,10 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "build_ablate")
-MASKS = [0, 1, 2, 3, 8, 16, 24, 27]
-EXTRA = {}   # name -> extra -D flags
+MASKS = [0, 32]
+EXTRA = {"nt64": ["-DWG_ABLATE=32", "-DWG_NTHREADS=64"], "nt128": ["-DWG_ABLATE=32", "-DWG_NTHREADS=128"],
+         "nt64_noobs": ["-DWG_ABLATE=48", "-DWG_NTHREADS=64"], "nt64_noinc": ["-DWG_ABLATE=34", "-DWG_NTHREADS=64"],
+         "nt64_skel": ["-DWG_ABLATE=59", "-DWG_NTHREADS=64"]}   # name -> extra -D flags
 
 
 def build():

@@ -1,0 +1,110 @@
+"""The C-ABI library loads, exports every symbol include/walker_hip.h declares, its ctypes structs match
+the C layout, and its host-side validation / planning work without a GPU (no kernel is launched)."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from walker_gym_amd import _lib, build
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "include", "walker_hip.h")
+
+
+@pytest.fixture(scope="module")
+def lib():
+    build.build()
+    return _lib.load()
+
+
+def declared_functions():
+    src = open(HDR).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(wg_\w+)\s*\(", src, re.M)))
+
+
+def test_every_declared_symbol_is_exported(lib):
+    names = declared_functions()
+    assert {"wg_step", "wg_observe", "wg_reset", "wg_abi_version", "wg_last_error"} <= set(names)
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (wg_\w+)", out))
+    assert set(names) <= exported, set(names) - exported
+    assert set(_lib.EXPORTS) <= exported
+
+
+def test_abi_version(lib):
+    assert lib.wg_abi_version() == _lib.ABI_VERSION
+    assert f"#define WG_ABI_VERSION {_lib.ABI_VERSION}" in open(HDR).read()
+
+
+def test_struct_layout_matches_header(tmp_path):
+    """Compile a C probe against the header and compare sizeof/offsetof with the ctypes mirrors."""
+    probe = tmp_path / "probe.c"
+    probe.write_text("""
+#include <stdio.h>
+#include <stddef.h>
+#include "walker_hip.h"
+#define F(T, m) printf(#T "." #m " %zu\\n", offsetof(T, m));
+int main(void) {
+  printf("wg_params %zu\\nwg_batch %zu\\nwg_outputs %zu\\nwg_edge %zu\\nwg_launch_info %zu\\n",
+         sizeof(wg_params), sizeof(wg_batch), sizeof(wg_outputs), sizeof(wg_edge), sizeof(wg_launch_info));
+  F(wg_batch, pos) F(wg_batch, edges) F(wg_batch, inc_off) F(wg_batch, muscle_bounds) F(wg_batch, contact)
+  F(wg_outputs, obs_step) F(wg_outputs, out_step) F(wg_params, in3d) F(wg_params, action_mode)
+  return 0;
+}
+""")
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), "-o", str(exe), str(probe)], check=True)
+    got = dict(line.rsplit(" ", 1) for line in subprocess.run([str(exe)], capture_output=True, text=True)
+               .stdout.strip().splitlines())
+    assert int(got["wg_params"]) == C.sizeof(_lib.WgParams)
+    assert int(got["wg_batch"]) == C.sizeof(_lib.WgBatch)
+    assert int(got["wg_outputs"]) == C.sizeof(_lib.WgOutputs)
+    assert int(got["wg_launch_info"]) == C.sizeof(_lib.WgLaunchInfo)
+    assert int(got["wg_edge"]) == 16
+    for key, cls in (("wg_batch", _lib.WgBatch), ("wg_outputs", _lib.WgOutputs), ("wg_params", _lib.WgParams)):
+        for full, off in got.items():
+            if full.startswith(key + "."):
+                assert getattr(cls, full.split(".", 1)[1]).offset == int(off), full
+
+
+def test_errors_without_gpu(lib):
+    p = _lib.WgParams()
+    assert lib.wg_step(None, C.byref(p), None, 0, 0, 0, None, 1, None, 0, None) == _lib.WG_EINVAL
+    assert b"null batch" in lib.wg_last_error()
+    b = _lib.WgBatch(N=4, M=0, K=1, A=0)
+    assert lib.wg_step(C.byref(b), C.byref(p), None, 0, 0, 0, None, 1, None, 0, None) == _lib.WG_EINVAL
+    b = _lib.WgBatch(N=4, M=2000, K=1, A=0)
+    assert lib.wg_step(C.byref(b), C.byref(p), None, 0, 0, 0, None, 1, None, 0, None) == _lib.WG_ERANGE
+    with pytest.raises(ValueError):
+        _lib.check(-1, "probe")
+
+
+def test_plan_ragged_host(lib):
+    rng = np.random.default_rng(0)
+    N = 500
+    Ms = rng.integers(2, 40, N); Ks = rng.integers(1, 80, N); As = Ks // 5
+    mo = np.concatenate([[0], np.cumsum(Ms)]).astype(np.int32)
+    eo = np.concatenate([[0], np.cumsum(Ks)]).astype(np.int32)
+    uo = np.concatenate([[0], np.cumsum(As)]).astype(np.int32)
+    plan = np.zeros(N + 1, np.int32)
+    nb = lib.wg_plan_ragged(mo.ctypes.data_as(C.c_void_p), eo.ctypes.data_as(C.c_void_p),
+                            uo.ctypes.data_as(C.c_void_p), N, plan.ctypes.data_as(C.c_void_p), N + 1)
+    assert nb > 0 and plan[0] == 0 and plan[nb] == N
+    for k in range(nb):
+        a, b = plan[k], plan[k + 1]
+        assert b > a
+        if b - a > 1:   # multi-walker blocks respect the caps
+            assert mo[b] - mo[a] <= 256 and eo[b] - eo[a] <= 512 and b - a <= 64
+
+
+def test_launch_geometry_canonical(lib):
+    b = _lib.WgBatch(N=65536, M=16, K=40, A=8, ragged=0)
+    for f in ("pos", "vel", "acc", "mass", "edges", "inc", "inc_off", "muscle_x", "steps"):
+        setattr(b, f, 16)   # non-null placeholders; nothing is dereferenced on the host
+    info = _lib.WgLaunchInfo()
+    assert lib.wg_launch_geometry(C.byref(b), C.byref(info)) == 0
+    assert info.threads == 256 and info.walkers_per_block == 16 and info.blocks == 4096
+    assert info.lds_bytes <= 32768   # five workgroups per CU (160 KiB LDS)

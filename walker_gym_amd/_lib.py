@@ -13,7 +13,7 @@ import threading
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libwalker_hip.so"
 LIB_PATH = os.path.join(HERE, LIB_NAME)
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 WG_EINVAL, WG_ERANGE, WG_EHIP = -1, -2, -3
 
@@ -31,9 +31,9 @@ class WgBatch(C.Structure):
                 ("ragged", C.c_int32),
                 ("mass_off", _vp), ("edge_off", _vp), ("muscle_off", _vp),
                 ("pos", _vp), ("vel", _vp), ("acc", _vp), ("mass", _vp),
-                ("edge_ij", _vp), ("edge_rest", _vp), ("edge_k", _vp), ("edge_c", _vp), ("edge_flags", _vp),
+                ("edges", _vp),
                 ("inc", _vp), ("inc_off", _vp),
-                ("muscle_x", _vp), ("muscle_lo", _vp), ("muscle_hi", _vp), ("muscle_stride", _vp),
+                ("muscle_x", _vp), ("muscle_bounds", _vp), ("muscle_stride", _vp),
                 ("steps", _vp), ("contact", _vp)]
 
 

@@ -46,9 +46,24 @@ int fail(int code, const char *fmt, ...) {
 constexpr int WG_MAX_M = 1024;      // numpy pairwise recursion unrolled 3 levels (pw_tree<3>)
 constexpr double CONFIG_R = 16e-36;  // gym/engine.py:9 Config.r (distance clamp, Python float)
 constexpr int EPL = 4;               // edges per lane per pass held in registers
-constexpr int NTHREADS = 256;
+#ifndef WG_NTHREADS
+#define WG_NTHREADS 256
+#endif
+constexpr int NTHREADS = WG_NTHREADS;
 #ifndef WG_ABLATE
 #define WG_ABLATE 0   // profiling builds only (scripts/ablate.py): bit k skips phase k; 0 in the product
+#endif
+// Diagnostic build only (-DWG_STAMPS): thread 0 of each workgroup records s_memrealtime (100 MHz) at
+// phase boundaries into g_stamps[block][8]; read back with wg_debug_stamps().  Never in the product.
+#ifdef WG_STAMPS
+__device__ unsigned long long g_stamps[65536 * 8];
+#define STAMP(k)                                                                                    \
+    do {                                                                                            \
+        if (threadIdx.x == 0 && blockIdx.x < 65536)                                                 \
+            g_stamps[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();                      \
+    } while (0)
+#else
+#define STAMP(k) do {} while (0)
 #endif
 
 // Float32 constants derived from wg_params exactly where numpy rounds the Python scalars.
@@ -66,6 +81,7 @@ struct Geo {
     int lds;
     float invM, invK, invA;    // uniform batches: 1/M, 1/K, 1/A for exact small-int division (fdiv)
     int tbytes;                // spring-term region, also the obs tile of uniform batches (aliased)
+    int lite;                  // register-reduction kernels: no LDS for acc, m, reduction terms, offsets
 };
 
 struct Carve {
@@ -81,30 +97,33 @@ struct Carve {
 
 __host__ __device__ inline int align16(int b) { return (b + 15) & ~15; }
 
-__host__ __device__ inline int carve_bytes(const Geo &g) {
-    return align16(g.tbytes) + 3 * align16(g.Pcap * 3 * 4) + align16(g.Pcap * 4) +
-           align16(g.Ecap * 3 * 4) + align16(g.Ecap * 4 + 16) + align16(g.Ucap * 4) + 3 * align16(g.Pcap * 4) +
-           align16(g.W * 8 * 4) + 3 * align16((g.W + 1) * 4);
+// one carve for host sizing and device pointers: `base == nullptr` only sums the sizes
+__host__ __device__ inline int carve_walk(const Geo &g, char *base, Carve *c) {
+    int b = 0;
+    auto take = [&](int bytes) { char *p = base ? base + b : nullptr; b += align16(bytes); return p; };
+    const int full = g.lite ? 0 : 1;
+    char *t = take(g.tbytes), *pos = take(g.Pcap * 12), *vel = take(g.Pcap * 12);
+    char *acc = take(full * g.Pcap * 12), *m = take(full * g.Pcap * 4), *df = take(g.Ecap * 12);
+    char *inc = take(g.Ecap * 4 + 16), *x = take(g.Ucap * 4);
+    char *nrm = take(full * g.Pcap * 4), *ke = take(full * g.Pcap * 4), *pe = take(full * g.Pcap * 4);
+    char *red = take(full * g.W * 32);
+    char *moff = take(full * (g.W + 1) * 4), *eoff = take(full * (g.W + 1) * 4), *uoff = take(full * (g.W + 1) * 4);
+    if (c) {
+        c->t = reinterpret_cast<double *>(t); c->pos = reinterpret_cast<float *>(pos);
+        c->vel = reinterpret_cast<float *>(vel); c->acc = reinterpret_cast<float *>(acc);
+        c->m = reinterpret_cast<float *>(m); c->df = reinterpret_cast<float *>(df);
+        c->inc = reinterpret_cast<uint32_t *>(inc); c->x = reinterpret_cast<float *>(x);
+        c->nrm = reinterpret_cast<float *>(nrm); c->ke = reinterpret_cast<float *>(ke);
+        c->pe = reinterpret_cast<float *>(pe); c->red = reinterpret_cast<float *>(red);
+        c->moff = reinterpret_cast<int *>(moff); c->eoff = reinterpret_cast<int *>(eoff);
+        c->uoff = reinterpret_cast<int *>(uoff);
+    }
+    return b;
 }
-
+__host__ __device__ inline int carve_bytes(const Geo &g) { return carve_walk(g, nullptr, nullptr); }
 __device__ inline Carve carve(char *s, const Geo &g) {
     Carve c;
-    int b = 0;
-    c.t = reinterpret_cast<double *>(s + b); b += align16(g.tbytes);
-    c.pos = reinterpret_cast<float *>(s + b); b += align16(g.Pcap * 3 * 4);
-    c.vel = reinterpret_cast<float *>(s + b); b += align16(g.Pcap * 3 * 4);
-    c.acc = reinterpret_cast<float *>(s + b); b += align16(g.Pcap * 3 * 4);
-    c.m = reinterpret_cast<float *>(s + b); b += align16(g.Pcap * 4);
-    c.df = reinterpret_cast<float *>(s + b); b += align16(g.Ecap * 3 * 4);
-    c.inc = reinterpret_cast<uint32_t *>(s + b); b += align16(g.Ecap * 4 + 16);
-    c.x = reinterpret_cast<float *>(s + b); b += align16(g.Ucap * 4);
-    c.nrm = reinterpret_cast<float *>(s + b); b += align16(g.Pcap * 4);
-    c.ke = reinterpret_cast<float *>(s + b); b += align16(g.Pcap * 4);
-    c.pe = reinterpret_cast<float *>(s + b); b += align16(g.Pcap * 4);
-    c.red = reinterpret_cast<float *>(s + b); b += align16(g.W * 8 * 4);
-    c.moff = reinterpret_cast<int *>(s + b); b += align16((g.W + 1) * 4);
-    c.eoff = reinterpret_cast<int *>(s + b); b += align16((g.W + 1) * 4);
-    c.uoff = reinterpret_cast<int *>(s + b); b += align16((g.W + 1) * 4);
+    carve_walk(g, s, &c);
     return c;
 }
 
@@ -180,6 +199,13 @@ __device__ inline int fdiv(int idx, int d, float inv) {
 //    final correction step: y within 1/2 ulp of 1/b and q within 1 ulp of a/b -> correctly rounded).
 // Non-finite operands take the plain expression (the correction would turn inf into NaN).
 __device__ inline float fdiv_exact(float x, double y) { return (float)((double)x * y); }
+//  * float x / float m == fmaf(fmaf(-q, m, x), yf, q) with yf = RN32(1/m) = (float)RN64(1/m),
+//    q = RN32(x*yf): the same Markstein step in binary32 (3 f32 ops, no f64 issue slots).
+__device__ inline float fdiv_mk(float x, float m, float yf) {
+    const float q = x * yf;
+    if (!__builtin_isfinite(q) || yf == 0.f) return q;
+    return __builtin_fmaf(__builtin_fmaf(-q, m, x), yf, q);
+}
 __device__ inline double ddiv_exact(double a, double b, double y) {
     const double q = a * y;
     if (!__builtin_isfinite(q) || y == 0.0) return q;
@@ -207,17 +233,53 @@ __device__ inline void stage_out(float *__restrict__ dst, const float *src, int 
     }
 }
 
-struct EdgeRec { uint32_t ij; float rest, k, c; uint32_t flag; };
+// one 16-B spring record (wg_edge): ij = i | j << 16 | string << 31
+struct EdgeRec { uint32_t ij; float rest, k, c; };
+__device__ inline EdgeRec load_edge(const wg_edge *__restrict__ e, size_t i) {
+    const uint4 v = reinterpret_cast<const uint4 *>(e)[i];
+    return EdgeRec{v.x, __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w)};
+}
+__device__ inline int edge_i(uint32_t ij) { return (int)(ij & 0x7fffu); }
+__device__ inline int edge_j(uint32_t ij) { return (int)((ij >> 16) & 0x7fffu); }
+__device__ inline bool edge_string(uint32_t ij) { return (ij >> 31) != 0u; }
+
+// ------------------------------------------------------------------ cross-lane reductions
+// A walker's M masses are M adjacent lanes of one wave when M divides 64 (uniform batches): numpy's
+// summation orders are then reproduced in registers with ds_bpermute shuffles — no LDS round trip,
+// no extra barrier (north_star: "wavefront shuffles for per-walker reductions").
+__device__ inline float lane_get(float v, int src) { return __shfl(v, src, 64); }
+
+// sequential float sum x_0 + x_1 + ... over the walker's M lanes (base = its first lane)
+__device__ inline float seq_sum_lanes(float x, int base, int M) {
+    float r = 0.f;
+    for (int q = 0; q < M; q++) r += lane_get(x, base + q);
+    return r;
+}
+// numpy pairwise sum over the walker's M lanes (M divides 64): < 8 sequential; otherwise 8 interleaved
+// partial sums r_j = x_j + x_{j+8} + ... then ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) — the xor-1/2/4
+// butterflies form exactly that tree (IEEE addition is commutative); M % 8 == 0, no remainder loop.
+__device__ inline float pw_sum_lanes(float x, int base, int M, int lane) {
+    if (M < 8) return seq_sum_lanes(x, base, M);
+    const int j = (lane - base) & 7;
+    float r = lane_get(x, base + j);
+    for (int k = 8; k < M; k += 8) r += lane_get(x, base + j + k);
+    r = r + __shfl_xor(r, 1, 64);
+    r = r + __shfl_xor(r, 2, 64);
+    r = r + __shfl_xor(r, 4, 64);
+    return r;
+}
 
 // ------------------------------------------------------------------ the step kernel
 // STEP = false: observe only (reset path).  RAGGED: CSR offsets + block plan.  IN3D: obs layout.
-template <bool STEP, bool RAGGED, bool IN3D, int PWD>
+// PWD: pairwise-sum recursion depth (0: M <= 128).  SHFL: register reductions (uniform, M | 64).
+template <bool STEP, bool RAGGED, bool IN3D, int PWD, bool SHFL>
 __global__ __launch_bounds__(NTHREADS) void walker_step_kernel(
     wg_batch b, KParams kp, const float *__restrict__ action, int action_cols, int action_stride,
     wg_outputs o, const int32_t *__restrict__ plan, Geo geo) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     Carve s = carve(smem, geo);
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63;
+    STAMP(0);
 
     // ---- this workgroup's walker range and flat slices
     int w0, w1;
@@ -242,8 +304,8 @@ __global__ __launch_bounds__(NTHREADS) void walker_step_kernel(
     // ================= phase 0: issue every global load of the tile =================
     stage_in<float4>(s.pos, b.pos + 3 * (size_t)P0, 3 * nP, tid);
     stage_in<float4>(s.vel, b.vel + 3 * (size_t)P0, 3 * nP, tid);
-    if (!STEP) stage_in<float4>(s.acc, b.acc + 3 * (size_t)P0, 3 * nP, tid);
-    stage_in<float4>(s.m, b.mass + P0, nP, tid);
+    if (!STEP && !SHFL) stage_in<float4>(s.acc, b.acc + 3 * (size_t)P0, 3 * nP, tid);
+    if (!SHFL) stage_in<float4>(s.m, b.mass + P0, nP, tid);
     if (STEP && nE > 0)
         stage_in<uint4>(s.inc, reinterpret_cast<const uint32_t *>(b.inc) + E0, nE, tid);
 
@@ -253,39 +315,38 @@ __global__ __launch_bounds__(NTHREADS) void walker_step_kernel(
 #pragma unroll
         for (int it = 0; it < EPL; it++) {
             const int le = tid + it * NTHREADS;
-            if (le < nE) {
-                er[it].ij = b.edge_ij[E0 + le];
-                er[it].rest = b.edge_rest[E0 + le];
-                er[it].k = b.edge_k[E0 + le];
-                er[it].c = b.edge_c[E0 + le];
-                er[it].flag = b.edge_flags ? b.edge_flags[E0 + le] : 0u;
-            }
+            if (le < nE) er[it] = load_edge(b.edges, E0 + le);
         }
     }
     // muscles of this lane (first pass) -> registers
     float mu_x = 0.f, mu_lo = 0.f, mu_hi = 0.f, mu_st = 0.f, mu_a = 0.f;
     int mu_ua = 0, mu_wl = 0;
     if (tid < nU) {
-        if (RAGGED) { mu_wl = 0; mu_ua = 0; }
-        else { mu_wl = fdiv(tid, b.A, geo.invA); mu_ua = tid - mu_wl * b.A; }
+        if (!RAGGED) { mu_wl = fdiv(tid, b.A, geo.invA); mu_ua = tid - mu_wl * b.A; }
         mu_x = b.muscle_x[U0 + tid];
         if (STEP && action) {
-            mu_lo = b.muscle_lo[U0 + tid];
-            mu_hi = b.muscle_hi[U0 + tid];
+            const float2 bd = reinterpret_cast<const float2 *>(b.muscle_bounds)[U0 + tid];
+            mu_lo = bd.x; mu_hi = bd.y;
             if (kp.action_mode == 1) mu_st = b.muscle_stride[U0 + tid];
             if (!RAGGED && mu_ua < action_cols) mu_a = action[(size_t)(w0 + mu_wl) * action_stride + mu_ua];
         }
     }
-    // per-walker step counter
-    int wsteps = 0;
-    if (tid < nw) wsteps = b.steps[w0 + tid];
-    if (RAGGED) __syncthreads();   // walker offsets visible before lanes locate their walker
-
-    // this lane's mass (first pass): walker, base, incidence offsets
+    // this lane's mass (first pass): walker, mass, incidence offsets, step counter
     int my_wl = 0, my_lm = 0;
-    if (tid < nP) {
-        if (RAGGED) { my_wl = locate(s.moff, nw, tid); my_lm = s.moff[my_wl]; }
-        else { my_wl = fdiv(tid, b.M, geo.invM); my_lm = my_wl * b.M; }
+    if (!RAGGED && tid < nP) { my_wl = fdiv(tid, b.M, geo.invM); my_lm = my_wl * b.M; }
+    float my_m = 0.f;
+    int wsteps = 0;
+    if (SHFL) {
+        if (tid < nP) {
+            my_m = b.mass[P0 + tid];
+            if (tid == my_lm) wsteps = b.steps[w0 + my_wl];
+        }
+    } else if (tid < nw) {
+        wsteps = b.steps[w0 + tid];
+    }
+    if (RAGGED) {
+        __syncthreads();   // walker offsets visible before lanes locate their walker
+        if (tid < nP) { my_wl = locate(s.moff, nw, tid); my_lm = s.moff[my_wl]; }
     }
     int io0 = 0, io1 = 0;
     if (STEP && tid < nP) {
@@ -308,7 +369,8 @@ __global__ __launch_bounds__(NTHREADS) void walker_step_kernel(
                 float lo = mu_lo, hi = mu_hi, st = mu_st, a = mu_a;
                 if (!first || RAGGED) {
                     if (!first) {
-                        lo = b.muscle_lo[U0 + u]; hi = b.muscle_hi[U0 + u];
+                        const float2 bd = reinterpret_cast<const float2 *>(b.muscle_bounds)[U0 + u];
+                        lo = bd.x; hi = bd.y;
                         if (kp.action_mode == 1) st = b.muscle_stride[U0 + u];
                     }
                     a = action[(size_t)(w0 + wl) * action_stride + ua];
@@ -323,7 +385,11 @@ __global__ __launch_bounds__(NTHREADS) void walker_step_kernel(
         s.x[u] = x;
     }
     __syncthreads();
+    STAMP(1);
 
+    // registers of this lane's (first) mass after the physics: feed the SHFL reductions and obs
+    float px = 0.f, py = 0.f, pz = 0.f, vx = 0.f, vy = 0.f, vz = 0.f, ax = 0.f, ay = 0.f, az = 0.f;
+    float nv = 0.f, ke = 0.f, pe = 0.f;
     if (STEP) {
         // ================= 2. edge phase =================
         // spring (gym/engine.py:78-102) + damping (gym/optimized_walker.py:92-106)
@@ -332,17 +398,10 @@ __global__ __launch_bounds__(NTHREADS) void walker_step_kernel(
             for (int it = 0; it < EPL; it++) {
                 const int le = tid + (pass * EPL + it) * NTHREADS;
                 if (le >= nE) break;
-                EdgeRec e;
-                if (pass == 0) {
-                    e = er[it];
-                } else {
-                    e.ij = b.edge_ij[E0 + le]; e.rest = b.edge_rest[E0 + le];
-                    e.k = b.edge_k[E0 + le]; e.c = b.edge_c[E0 + le];
-                    e.flag = b.edge_flags ? b.edge_flags[E0 + le] : 0u;
-                }
+                const EdgeRec e = (pass == 0) ? er[it] : load_edge(b.edges, E0 + le);
                 if (WG_ABLATE & 1) {
                     s.t[3 * le] = e.rest; s.t[3 * le + 1] = e.k; s.t[3 * le + 2] = e.c;
-                    s.df[3 * le] = (float)e.ij; s.df[3 * le + 1] = 0.f; s.df[3 * le + 2] = 0.f;
+                    s.df[3 * le] = (float)(e.ij & 0xffu); s.df[3 * le + 1] = 0.f; s.df[3 * le + 2] = 0.f;
                     continue;
                 }
                 int lm, ew, Aw, ub;
@@ -353,7 +412,7 @@ __global__ __launch_bounds__(NTHREADS) void walker_step_kernel(
                     const int wl = fdiv(le, b.K, geo.invK);
                     lm = wl * b.M; ew = le - wl * b.K; Aw = b.A; ub = wl * b.A;
                 }
-                const int i = lm + (int)(e.ij & 0xffffu), j = lm + (int)(e.ij >> 16);
+                const int i = lm + edge_i(e.ij), j = lm + edge_j(e.ij);
                 const float x = (ew < Aw) ? s.x[ub + ew] : e.rest;
                 const float pix = s.pos[3 * i], piy = s.pos[3 * i + 1], piz = s.pos[3 * i + 2];
                 const float pjx = s.pos[3 * j], pjy = s.pos[3 * j + 1], pjz = s.pos[3 * j + 2];
@@ -361,27 +420,27 @@ __global__ __launch_bounds__(NTHREADS) void walker_step_kernel(
                 const float vjx = s.vel[3 * j], vjy = s.vel[3 * j + 1], vjz = s.vel[3 * j + 2];
                 const float cur = np_norm3(pix - pjx, piy - pjy, piz - pjz);   // engine.py:86
                 const float dx = cur - x;                                       // engine.py:96
-                double t0, t1, t2;
-                float d0 = pjx - pix, d1 = pjy - piy, d2 = pjz - piz;
+                const float r0 = pjx - pix, r1 = pjy - piy, r2 = pjz - piz;     // other.pos - self.pos
                 double dist = (double)cur;                                      // engine.py:73
                 if (CONFIG_R > dist) dist = CONFIG_R;                           // max(distance, r)
                 const double yc = 1.0 / dist;
-                const bool unit = cur > 0.f;                                    // optimized_walker.py:93
-                if (unit) {
+                float d0 = r0, d1 = r1, d2 = r2;
+                if (cur > 0.f) {                                                // optimized_walker.py:93
                     if ((double)cur == dist) {
-                        d0 = fdiv_exact(d0, yc); d1 = fdiv_exact(d1, yc); d2 = fdiv_exact(d2, yc);
+                        const float ycf = (float)yc;
+                        d0 = fdiv_mk(r0, cur, ycf); d1 = fdiv_mk(r1, cur, ycf); d2 = fdiv_mk(r2, cur, ycf);
                     } else {
-                        d0 = d0 / cur; d1 = d1 / cur; d2 = d2 / cur;
+                        d0 = r0 / cur; d1 = r1 / cur; d2 = r2 / cur;
                     }
                 }
+                double t0, t1, t2;
                 if (kp.spring_mode == 1) {
                     // G2 element (gym/optimized_walker.py:48-60): float32 force, inverted sign.
                     const float fs = (-dx) * e.k;
                     t0 = (double)(fs * d0); t1 = (double)(fs * d1); t2 = (double)(fs * d2);
                 } else {
-                    const float fsz = (dx < 0.f && (e.flag & 1u)) ? 0.f : (-dx) * e.k;   // engine.py:97-100
-                    const float nf = -fsz;                                                // engine.py:75
-                    const float r0 = pjx - pix, r1 = pjy - piy, r2 = pjz - piz;
+                    const float fsz = (dx < 0.f && edge_string(e.ij)) ? 0.f : (-dx) * e.k;   // engine.py:97-100
+                    const float nf = -fsz;                                                    // engine.py:75
                     t0 = ddiv_exact((double)(nf * r0), dist, yc);
                     t1 = ddiv_exact((double)(nf * r1), dist, yc);
                     t2 = ddiv_exact((double)(nf * r2), dist, yc);
@@ -393,25 +452,27 @@ __global__ __launch_bounds__(NTHREADS) void walker_step_kernel(
             }
         }
         __syncthreads();
+        STAMP(2);
 
         // ================= 3. mass phase: ordered accumulation, env forces, run1 =================
         const uint16_t *s_inc16 = reinterpret_cast<const uint16_t *>(s.inc);
         for (int lp = tid; lp < nP; lp += NTHREADS) {
             const bool first = (lp == tid);
-            int wl, lm, lb;
+            int wl, lm;
             if (first) { wl = my_wl; lm = my_lm; }
             else if (RAGGED) { wl = locate(s.moff, nw, lp); lm = s.moff[wl]; }
             else { wl = fdiv(lp, b.M, geo.invM); lm = wl * b.M; }
-            lb = RAGGED ? s.eoff[wl] : wl * b.K;
+            const int lb = RAGGED ? s.eoff[wl] : wl * b.K;
             int s0 = io0, s1 = io1;
             if (!first) {
                 const uint16_t *io = b.inc_off + (size_t)(P0 + lm) + (size_t)(w0 + wl);
                 s0 = io[lp - lm]; s1 = io[lp - lm + 1];
             }
-            const float mf = s.m[lp];
+            const float mf = SHFL ? my_m : s.m[lp];
             const double md = (double)mf;
             const double ym = 1.0 / md;      // one IEEE division per mass; every /m below is exact from it
-            float ax = 0.f, ay = 0.f, az = 0.f;
+            const float ymf = (float)ym;     // = RN32(1/m)
+            ax = 0.f; ay = 0.f; az = 0.f;
             for (int r = s0; r < ((WG_ABLATE & 2) ? s0 + 1 : s1); r++) {
                 const int ent = s_inc16[2 * lb + r];
                 const int le = lb + (ent >> 1);
@@ -420,9 +481,9 @@ __global__ __launch_bounds__(NTHREADS) void walker_step_kernel(
                 const float f0 = s.df[3 * le], f1 = s.df[3 * le + 1], f2 = s.df[3 * le + 2];
                 if (kp.spring_mode == 1) {
                     const float sg = end_j ? -1.f : 1.f;
-                    ax = ax + fdiv_exact(sg * (float)t0, ym);
-                    ay = ay + fdiv_exact(sg * (float)t1, ym);
-                    az = az + fdiv_exact(sg * (float)t2, ym);
+                    ax = ax + fdiv_mk(sg * (float)t0, mf, ymf);
+                    ay = ay + fdiv_mk(sg * (float)t1, mf, ymf);
+                    az = az + fdiv_mk(sg * (float)t2, mf, ymf);
                 } else {
                     // Point.forced with a float64 force: a = f32(f64(a) + t/m)   (engine.py:67,75)
                     const double sg = end_j ? -1.0 : 1.0;
@@ -432,23 +493,25 @@ __global__ __launch_bounds__(NTHREADS) void walker_step_kernel(
                 }
                 // damping: p1.forced(-damp_force); p2.forced(damp_force)  (optimized_walker.py:105-106)
                 const float sf = end_j ? 1.f : -1.f;
-                ax = ax + fdiv_exact(sf * f0, ym); ay = ay + fdiv_exact(sf * f1, ym); az = az + fdiv_exact(sf * f2, ym);
+                ax = ax + fdiv_mk(sf * f0, mf, ymf);
+                ay = ay + fdiv_mk(sf * f1, mf, ymf);
+                az = az + fdiv_mk(sf * f2, mf, ymf);
             }
-            float vx = s.vel[3 * lp], vy = s.vel[3 * lp + 1], vz = s.vel[3 * lp + 2];
-            float px = s.pos[3 * lp], py = s.pos[3 * lp + 1], pz = s.pos[3 * lp + 2];
-            const float zm = fdiv_exact(0.f, ym);   // the zero components of the env forces, divided by m
+            vx = s.vel[3 * lp]; vy = s.vel[3 * lp + 1]; vz = s.vel[3 * lp + 2];
+            px = s.pos[3 * lp]; py = s.pos[3 * lp + 1]; pz = s.pos[3 * lp + 2];
+            const float zm = fdiv_mk(0.f, mf, ymf);   // the zero components of the env forces, divided by m
             // gravity [0,-g,0]/m, damp -dampk*v/m  (gym/env.py:32-33, optimized_env.py:148-151)
-            ax = ax + zm; ay = ay + fdiv_exact(kp.neg_g, ym); az = az + zm;
-            ax = ax + fdiv_exact(kp.neg_dampk * vx, ym);
-            ay = ay + fdiv_exact(kp.neg_dampk * vy, ym);
-            az = az + fdiv_exact(kp.neg_dampk * vz, ym);
+            ax = ax + zm; ay = ay + fdiv_mk(kp.neg_g, mf, ymf); az = az + zm;
+            ax = ax + fdiv_mk(kp.neg_dampk * vx, mf, ymf);
+            ay = ay + fdiv_mk(kp.neg_dampk * vy, mf, ymf);
+            az = az + fdiv_mk(kp.neg_dampk * vz, mf, ymf);
             const float deep = py - kp.ground;
             const bool hit = deep < 0.f;                                     // optimized_env.py:154
             if (hit) {
-                ax = ax + zm; ay = ay + fdiv_exact(kp.neg_groundk * deep, ym); az = az + zm;
-                ax = ax + zm; ay = ay + fdiv_exact(kp.neg_grounddamp * vy, ym); az = az + zm;
+                ax = ax + zm; ay = ay + fdiv_mk(kp.neg_groundk * deep, mf, ymf); az = az + zm;
+                ax = ax + zm; ay = ay + fdiv_mk(kp.neg_grounddamp * vy, mf, ymf); az = az + zm;
                 const float ff = fabsf(deep) * kp.friction;                   // :168
-                ax = ax + fdiv_exact((-vx) * ff, ym); ay = ay + zm; az = az + fdiv_exact((-vz) * ff, ym);
+                ax = ax + fdiv_mk((-vx) * ff, mf, ymf); ay = ay + zm; az = az + fdiv_mk((-vz) * ff, mf, ymf);
             }
             if (b.contact) b.contact[P0 + lp] = (uint8_t)hit;
             // Point.run1 (gym/engine.py:174-178)
@@ -456,90 +519,143 @@ __global__ __launch_bounds__(NTHREADS) void walker_step_kernel(
             px = px + vx * kp.dt; py = py + vy * kp.dt; pz = pz + vz * kp.dt;
             s.pos[3 * lp] = px; s.pos[3 * lp + 1] = py; s.pos[3 * lp + 2] = pz;
             s.vel[3 * lp] = vx; s.vel[3 * lp + 1] = vy; s.vel[3 * lp + 2] = vz;
-            s.acc[3 * lp] = ax; s.acc[3 * lp + 1] = ay; s.acc[3 * lp + 2] = az;
-            // reduction terms of the new state: ‖v‖, m*‖v‖^2, f32(m*g)*(y-ground)
-            const float nv = np_norm3(vx, vy, vz);
-            s.nrm[lp] = nv;
-            s.ke[lp] = mf * (nv * nv);   // numpy's float32 ** 2 is libm powf: may differ by 1 ulp
-            s.pe[lp] = (float)(md * kp.g) * (py - kp.ground);
+            if (SHFL) {      // old_a straight from registers (no LDS copy in the register-reduction kernel)
+                float *ga = b.acc + 3 * ((size_t)P0 + lp);
+                ga[0] = ax; ga[1] = ay; ga[2] = az;
+            } else {
+                s.acc[3 * lp] = ax; s.acc[3 * lp + 1] = ay; s.acc[3 * lp + 2] = az;
+            }
+            // reduction terms of the new state: |v|, m*|v|^2, f32(m*g)*(y-ground)
+            nv = np_norm3(vx, vy, vz);
+            ke = mf * (nv * nv);   // numpy's float32 ** 2 is libm powf: may differ by 1 ulp
+            pe = (float)(md * kp.g) * (py - kp.ground);
+            if (!SHFL) { s.nrm[lp] = nv; s.ke[lp] = ke; s.pe[lp] = pe; }
         }
     } else {
         for (int lp = tid; lp < nP; lp += NTHREADS) {
-            const float mf = s.m[lp];
-            const float nv = np_norm3(s.vel[3 * lp], s.vel[3 * lp + 1], s.vel[3 * lp + 2]);
-            s.nrm[lp] = nv;
-            s.ke[lp] = mf * (nv * nv);
-            s.pe[lp] = (float)((double)mf * kp.g) * (s.pos[3 * lp + 1] - kp.ground);
+            const float mf = SHFL ? my_m : s.m[lp];
+            vx = s.vel[3 * lp]; vy = s.vel[3 * lp + 1]; vz = s.vel[3 * lp + 2];
+            px = s.pos[3 * lp]; py = s.pos[3 * lp + 1]; pz = s.pos[3 * lp + 2];
+            if (SHFL) {
+                const float *ga = b.acc + 3 * ((size_t)P0 + lp);
+                ax = ga[0]; ay = ga[1]; az = ga[2];
+            } else {
+                ax = s.acc[3 * lp]; ay = s.acc[3 * lp + 1]; az = s.acc[3 * lp + 2];
+            }
+            nv = np_norm3(vx, vy, vz);
+            ke = mf * (nv * nv);
+            pe = (float)((double)mf * kp.g) * (py - kp.ground);
+            if (!SHFL) { s.nrm[lp] = nv; s.ke[lp] = ke; s.pe[lp] = pe; }
+        }
+    }
+
+    // ================= per-walker reductions + outputs (gym/optimized_env.py:189-248) =================
+    float midx = 0.f, midy = 0.f, midz = 0.f;
+    const bool is_mass = tid < nP;
+    const int my_q = tid - my_lm;
+    if (SHFL) {
+        const int M = b.M;
+        const int gbase = (tid & ~63) + ((lane / M) * M);
+        const float sx = seq_sum_lanes(px, gbase, M), sy = seq_sum_lanes(py, gbase, M),
+                    sz = seq_sum_lanes(pz, gbase, M);
+        const float ysum = pw_sum_lanes(py, gbase, M, lane), vsum = pw_sum_lanes(nv, gbase, M, lane);
+        const float ksum = pw_sum_lanes(ke, gbase, M, lane), psum = pw_sum_lanes(pe, gbase, M, lane);
+        const unsigned long long gmask = (M == 64) ? ~0ull : (((1ull << M) - 1ull) << (gbase & 63));
+        // the collision penalty counts contacts of the NEW state (optimized_env.py:200 runs after run1)
+        const unsigned long long hb = __ballot(is_mass && (py - kp.ground < 0.f));
+        const unsigned long long sb = __ballot(is_mass && nv < 0.1f);
+        const int hits = __popcll(hb & gmask);
+        const bool all_stopped = (sb & gmask) == gmask;
+        const float fM = (float)M;
+        midx = sx / fM; midy = sy / fM; midz = sz / fM;
+        if (is_mass && my_q == 0) {
+            const size_t wg = (size_t)(w0 + my_wl);
+            int steps = wsteps;
+            if (STEP) { steps += 1; b.steps[wg] = steps; }
+            const float cy = ysum / fM;
+            if (o.reward) {
+                const float vpen = (-(vsum / fM)) * 0.1f;
+                o.reward[wg] = (cy + vpen) + (float)(-(double)hits * 0.5);
+            }
+            if (o.done) {
+                int done = steps >= kp.max_steps;
+                if (!done && cy < kp.done_y) done = 1;
+                if (!done && steps > 100) done = all_stopped;
+                o.done[wg] = (uint8_t)done;
+            }
+            if (o.centroid) { o.centroid[3 * wg] = midx; o.centroid[3 * wg + 1] = midy; o.centroid[3 * wg + 2] = midz; }
+            if (o.energy) o.energy[wg] = 0.5f * ksum + psum;
         }
     }
     __syncthreads();
+    STAMP(3);
 
-    // ================= write back + per-walker reductions =================
     if (STEP) {
         stage_out(b.pos + 3 * (size_t)P0, s.pos, 3 * nP, tid);
         stage_out(b.vel + 3 * (size_t)P0, s.vel, 3 * nP, tid);
-        stage_out(b.acc + 3 * (size_t)P0, s.acc, 3 * nP, tid);
+        if (!SHFL) stage_out(b.acc + 3 * (size_t)P0, s.acc, 3 * nP, tid);
     }
-    // 8 lanes per walker, numpy's summation orders (see oracle/walker_oracle.c walker_observe):
-    // r 0-2 sequential sums of pos[:, r] (getstat mid / info centroid), r 3 pairwise sum of y
-    // (np.mean), r 4-6 pairwise sums of |v|, m|v|^2, m*g*(y-ground), r 7 contact count + all-stopped.
-    for (int idx = tid; idx < ((WG_ABLATE & 8) ? 0 : nw * 8); idx += NTHREADS) {
-        const int wl = idx >> 3, r = idx & 7;
-        const int lm = RAGGED ? s.moff[wl] : wl * b.M;
-        const int M = RAGGED ? s.moff[wl + 1] - lm : b.M;
-        float v;
-        if (r == 7) {
-            int hits = 0, all = 1;
-            for (int q = 0; q < M; q++) {
-                hits += (s.pos[3 * (lm + q) + 1] - kp.ground < 0.f);
-                all &= (s.nrm[lm + q] < 0.1f);
-            }
-            v = __int_as_float((hits << 1) | all);
-        } else {
-            const float *src = r < 3 ? s.pos + 3 * lm + r
-                             : r == 3 ? s.pos + 3 * lm + 1
-                             : r == 4 ? s.nrm + lm : r == 5 ? s.ke + lm : s.pe + lm;
-            const int st = r <= 3 ? 3 : 1;
-            if (r < 3) {
-                v = 0.f;
-                for (int q = 0; q < M; q++) v += src[q * st];
+    if (!SHFL) {
+        // 8 lanes per walker, numpy's summation orders (see oracle/walker_oracle.c walker_observe):
+        // r 0-2 sequential sums of pos[:, r] (getstat mid / info centroid), r 3 pairwise sum of y
+        // (np.mean), r 4-6 pairwise sums of |v|, m|v|^2, m*g*(y-ground), r 7 contact count + all-stopped.
+        for (int idx = tid; idx < ((WG_ABLATE & 8) ? 0 : nw * 8); idx += NTHREADS) {
+            const int wl = idx >> 3, r = idx & 7;
+            const int lm = RAGGED ? s.moff[wl] : wl * b.M;
+            const int M = RAGGED ? s.moff[wl + 1] - lm : b.M;
+            float v;
+            if (r == 7) {
+                int hits = 0, all = 1;
+                for (int q = 0; q < M; q++) {
+                    hits += (s.pos[3 * (lm + q) + 1] - kp.ground < 0.f);
+                    all &= (s.nrm[lm + q] < 0.1f);
+                }
+                v = __int_as_float((hits << 1) | all);
             } else {
-                v = np_pairwise<PWD>(src, M, st);
+                const float *src = r < 3 ? s.pos + 3 * lm + r
+                                 : r == 3 ? s.pos + 3 * lm + 1
+                                 : r == 4 ? s.nrm + lm : r == 5 ? s.ke + lm : s.pe + lm;
+                const int st = r <= 3 ? 3 : 1;
+                if (r < 3) {
+                    v = 0.f;
+                    for (int q = 0; q < M; q++) v += src[q * st];
+                } else {
+                    v = np_pairwise<PWD>(src, M, st);
+                }
             }
+            s.red[idx] = v;
         }
-        s.red[idx] = v;
-    }
-    __syncthreads();
-
-    // ================= per-walker outputs (gym/optimized_env.py:189-248) =================
-    if (tid < nw) {
-        const int wl = tid;
-        const int lm = RAGGED ? s.moff[wl] : wl * b.M;
-        const int M = RAGGED ? s.moff[wl + 1] - lm : b.M;
-        const size_t wg = (size_t)(w0 + wl);
-        const float fM = (float)M;
-        const float *rd = s.red + 8 * wl;
-        const float cy = rd[3] / fM;
-        const int packed = __float_as_int(rd[7]);
-        const int hits = packed >> 1, all = packed & 1;
-        int steps = wsteps;
-        if (STEP) { steps += 1; b.steps[wg] = steps; }
-        if (o.reward) {
-            const float av = rd[4] / fM;
-            const float vpen = (-av) * 0.1f;
-            const float cpen = (float)(-(double)hits * 0.5);
-            o.reward[wg] = (cy + vpen) + cpen;
+        __syncthreads();
+        STAMP(4);
+        if (tid < nw) {
+            const int wl = tid;
+            const int lm = RAGGED ? s.moff[wl] : wl * b.M;
+            const int M = RAGGED ? s.moff[wl + 1] - lm : b.M;
+            const size_t wg = (size_t)(w0 + wl);
+            const float fM = (float)M;
+            const float *rd = s.red + 8 * wl;
+            const float cy = rd[3] / fM;
+            const int packed = __float_as_int(rd[7]);
+            const int hits = packed >> 1, all = packed & 1;
+            int steps = wsteps;
+            if (STEP) { steps += 1; b.steps[wg] = steps; }
+            if (o.reward) {
+                const float av = rd[4] / fM;
+                const float vpen = (-av) * 0.1f;
+                const float cpen = (float)(-(double)hits * 0.5);
+                o.reward[wg] = (cy + vpen) + cpen;
+            }
+            if (o.done) {
+                int done = steps >= kp.max_steps;
+                if (!done && cy < kp.done_y) done = 1;
+                if (!done && steps > 100) done = all;
+                o.done[wg] = (uint8_t)done;
+            }
+            if (o.centroid) {
+                o.centroid[3 * wg] = rd[0] / fM; o.centroid[3 * wg + 1] = rd[1] / fM; o.centroid[3 * wg + 2] = rd[2] / fM;
+            }
+            if (o.energy) o.energy[wg] = 0.5f * rd[5] + rd[6];
         }
-        if (o.done) {
-            int done = steps >= kp.max_steps;
-            if (!done && cy < kp.done_y) done = 1;
-            if (!done && steps > 100) done = all;
-            o.done[wg] = (uint8_t)done;
-        }
-        if (o.centroid) {
-            o.centroid[3 * wg] = rd[0] / fM; o.centroid[3 * wg + 1] = rd[1] / fM; o.centroid[3 * wg + 2] = rd[2] / fM;
-        }
-        if (o.energy) o.energy[wg] = 0.5f * rd[5] + rd[6];
     }
 
     // ================= observation rows: Creature.getstat (gym/optimized_walker.py:129-162) =================
@@ -551,21 +667,51 @@ __global__ __launch_bounds__(NTHREADS) void walker_step_kernel(
         // them out as one contiguous 16-B-store block; ragged batches write rows directly.
         float *tile = RAGGED ? nullptr : reinterpret_cast<float *>(s.t);
         const int nmid = kp.conmid ? 3 : 0;
-        // per-mass block of 3*d values: (pos - mid)*pk, v*vk, old_a*ak
-        for (int lp = tid; lp < nP; lp += NTHREADS) {
-            int wl, lm;
-            if (lp == tid) { wl = my_wl; lm = my_lm; }
-            else if (RAGGED) { wl = locate(s.moff, nw, lp); lm = s.moff[wl]; }
-            else { wl = fdiv(lp, b.M, geo.invM); lm = wl * b.M; }
-            const int M = RAGGED ? s.moff[wl + 1] - lm : b.M;
-            const float fM = (float)M;
-            float *row = (RAGGED ? ob : tile) + (size_t)wl * stride + per * (lp - lm);
+        if (SHFL) {
+            if (is_mass) {
+                float *row = tile + (size_t)my_wl * stride + per * my_q;
+                const float pm[3] = {px, py, pz}, vm[3] = {vx, vy, vz}, am[3] = {ax, ay, az};
+                const float mm[3] = {midx, midy, midz};
 #pragma unroll
-            for (int c = 0; c < d; c++) {
-                const float pv = s.pos[3 * lp + c];
-                row[c] = kp.midform ? (pv - s.red[8 * wl + c] / fM) * kp.pk : pv * kp.pk;
-                row[d + c] = s.vel[3 * lp + c] * kp.vk;
-                row[2 * d + c] = s.acc[3 * lp + c] * kp.ak;
+                for (int c = 0; c < d; c++) {
+                    row[c] = kp.midform ? (pm[c] - mm[c]) * kp.pk : pm[c] * kp.pk;
+                    row[d + c] = vm[c] * kp.vk;
+                    row[2 * d + c] = am[c] * kp.ak;
+                }
+                if (my_q == 0 && nmid) {
+                    float *wrow = tile + (size_t)my_wl * stride + per * b.M;
+                    wrow[0] = kp.midform ? midx : 0.f; wrow[1] = kp.midform ? midy : 0.f; wrow[2] = kp.midform ? midz : 0.f;
+                }
+                if (my_q == 0)
+                    for (int r = per * b.M + nmid + b.A; r < stride; r++) tile[(size_t)my_wl * stride + r] = 0.f;
+            }
+        } else {
+            // per-mass block of 3*d values: (pos - mid)*pk, v*vk, old_a*ak
+            for (int lp = tid; lp < nP; lp += NTHREADS) {
+                int wl, lm;
+                if (lp == tid) { wl = my_wl; lm = my_lm; }
+                else if (RAGGED) { wl = locate(s.moff, nw, lp); lm = s.moff[wl]; }
+                else { wl = fdiv(lp, b.M, geo.invM); lm = wl * b.M; }
+                const int M = RAGGED ? s.moff[wl + 1] - lm : b.M;
+                const float fM = (float)M;
+                float *row = (RAGGED ? ob : tile) + (size_t)wl * stride + per * (lp - lm);
+#pragma unroll
+                for (int c = 0; c < d; c++) {
+                    const float pv = s.pos[3 * lp + c];
+                    row[c] = kp.midform ? (pv - s.red[8 * wl + c] / fM) * kp.pk : pv * kp.pk;
+                    row[d + c] = s.vel[3 * lp + c] * kp.vk;
+                    row[2 * d + c] = s.acc[3 * lp + c] * kp.ak;
+                }
+            }
+            // conmid columns and zero padding of short (ragged) rows
+            for (int wl = tid; wl < nw; wl += NTHREADS) {
+                const int lm = RAGGED ? s.moff[wl] : wl * b.M;
+                const int M = RAGGED ? s.moff[wl + 1] - lm : b.M;
+                const int A = RAGGED ? s.uoff[wl + 1] - s.uoff[wl] : b.A;
+                float *row = (RAGGED ? ob : tile) + (size_t)wl * stride;
+                if (nmid)
+                    for (int c = 0; c < 3; c++) row[per * M + c] = kp.midform ? s.red[8 * wl + c] / (float)M : 0.f;
+                for (int r = per * M + nmid + A; r < stride; r++) row[r] = 0.f;
             }
         }
         // muscle rest lengths x*mk
@@ -575,21 +721,13 @@ __global__ __launch_bounds__(NTHREADS) void walker_step_kernel(
             else { wl = fdiv(u, b.A, geo.invA); ua = u - wl * b.A; M = b.M; }
             (RAGGED ? ob : tile)[(size_t)wl * stride + per * M + nmid + ua] = s.x[u] * kp.mk;
         }
-        // conmid columns and zero padding of short (ragged) rows
-        for (int wl = tid; wl < nw; wl += NTHREADS) {
-            const int lm = RAGGED ? s.moff[wl] : wl * b.M;
-            const int M = RAGGED ? s.moff[wl + 1] - lm : b.M;
-            const int A = RAGGED ? s.uoff[wl + 1] - s.uoff[wl] : b.A;
-            float *row = (RAGGED ? ob : tile) + (size_t)wl * stride;
-            if (nmid)
-                for (int c = 0; c < 3; c++) row[per * M + c] = kp.midform ? s.red[8 * wl + c] / (float)M : 0.f;
-            for (int r = per * M + nmid + A; r < stride; r++) row[r] = 0.f;
-        }
         if (!RAGGED) {
             __syncthreads();
+            STAMP(5);
             stage_out(ob, tile, nw * stride, tid);
         }
     }
+    STAMP(6);
 }
 
 // reset: v += noise (x, y, z if in3d), steps = 0 (PhysicsEnv.reset, gym/optimized_env.py:53-68)
@@ -645,8 +783,8 @@ int validate(const wg_batch *b) {
     if (b->M > WG_MAX_M) return fail(WG_ERANGE, "M=%d > %d masses per walker", b->M, WG_MAX_M);
     if (!b->pos || !b->vel || !b->acc || !b->mass || !b->steps || !b->muscle_x)
         return fail(WG_EINVAL, "missing state pointer");
-    if (b->K > 0 && (!b->edge_ij || !b->edge_rest || !b->edge_k || !b->edge_c || !b->inc || !b->inc_off))
-        return fail(WG_EINVAL, "missing edge pointer");
+    if (b->K > 0 && (!b->edges || !b->inc || !b->inc_off)) return fail(WG_EINVAL, "missing edge pointer");
+    if (b->M > 32767) return fail(WG_ERANGE, "M=%d exceeds the 15-bit edge endpoint encoding", b->M);
     if (!b->inc_off) return fail(WG_EINVAL, "missing inc_off");
     if (b->ragged && (!b->mass_off || !b->edge_off || !b->muscle_off))
         return fail(WG_EINVAL, "ragged batch without offsets");
@@ -662,9 +800,11 @@ Geo uniform_geo(const wg_batch *b, int obs_stride) {
     if (b->K > 0) W = std::max(1, std::min(W, EPL * NTHREADS / std::max(1, b->K)));
     while (W > 1 && (b->N + W - 1) / W < 512) W = std::max(1, W / 2);
     g.W = W;
+    const bool shfl_shape = b->M <= 64 && (64 % b->M) == 0 && !(WG_ABLATE & 64);
     for (;;) {
         g.Pcap = g.W * b->M; g.Ecap = g.W * b->K; g.Ucap = g.W * b->A;
         g.tbytes = std::max(g.Ecap * 3 * 8, g.W * std::max(0, obs_stride) * 4);
+        g.lite = (shfl_shape && g.W * b->M <= NTHREADS) ? 1 : 0;
         g.lds = carve_bytes(g);
         if (g.lds <= 64 * 1024 || g.W == 1) break;
         g.W = std::max(1, g.W / 2);
@@ -683,32 +823,41 @@ Geo ragged_geo(const wg_batch *b) {
     g.Ecap = std::max(RAG_E, b->K);
     g.Ucap = std::max(RAG_U, b->A);
     g.tbytes = g.Ecap * 3 * 8;
+    g.lite = 0;
     g.lds = carve_bytes(g);
     g.invM = g.invK = g.invA = 0.f;
     return g;
 }
 
-template <bool STEP, bool RAGGED, bool IN3D, int PWD>
+template <bool STEP, bool RAGGED, bool IN3D, int PWD, bool SHFL>
 int launch(const wg_batch *b, const KParams &kp, const float *action, int cols, int astride,
            const wg_outputs &o, const int32_t *plan, int blocks, const Geo &g, hipStream_t stream) {
     if (g.lds > LDS_LIMIT) return fail(WG_ERANGE, "workgroup needs %d B of LDS (> 160 KiB)", g.lds);
-    hipLaunchKernelGGL((walker_step_kernel<STEP, RAGGED, IN3D, PWD>), dim3(blocks), dim3(g.threads), g.lds, stream,
+    hipLaunchKernelGGL((walker_step_kernel<STEP, RAGGED, IN3D, PWD, SHFL>), dim3(blocks), dim3(g.threads), g.lds, stream,
                        *b, kp, action, cols, astride, o, plan, g);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(WG_EHIP, "launch failed: %s", hipGetErrorString(e));
     return 0;
 }
 
+// register (shuffle) reductions: every walker's masses are adjacent lanes of one wave
+bool shfl_ok(const wg_batch *b, const Geo &g) { return !b->ragged && g.lite; }
+
 template <bool STEP, int PWD>
 int dispatch2(const wg_batch *b, const KParams &kp, bool in3d, const float *a, int cols, int astride,
               const wg_outputs &o, const int32_t *plan, int blocks, const Geo &g, hipStream_t st) {
     if (b->ragged) {
-        return in3d ? launch<STEP, true, true, PWD>(b, kp, a, cols, astride, o, plan, blocks, g, st)
-                    : launch<STEP, true, false, PWD>(b, kp, a, cols, astride, o, plan, blocks, g, st);
+        return in3d ? launch<STEP, true, true, PWD, false>(b, kp, a, cols, astride, o, plan, blocks, g, st)
+                    : launch<STEP, true, false, PWD, false>(b, kp, a, cols, astride, o, plan, blocks, g, st);
     }
-    return in3d ? launch<STEP, false, true, PWD>(b, kp, a, cols, astride, o, plan, blocks, g, st)
-                : launch<STEP, false, false, PWD>(b, kp, a, cols, astride, o, plan, blocks, g, st);
+    if (PWD == 0 && shfl_ok(b, g)) {
+        return in3d ? launch<STEP, false, true, 0, true>(b, kp, a, cols, astride, o, plan, blocks, g, st)
+                    : launch<STEP, false, false, 0, true>(b, kp, a, cols, astride, o, plan, blocks, g, st);
+    }
+    return in3d ? launch<STEP, false, true, PWD, false>(b, kp, a, cols, astride, o, plan, blocks, g, st)
+                : launch<STEP, false, false, PWD, false>(b, kp, a, cols, astride, o, plan, blocks, g, st);
 }
+// register (shuffle) reductions: every walker's masses are adjacent lanes of one wave
 template <bool STEP>
 int dispatch(const wg_batch *b, const KParams &kp, bool in3d, const float *a, int cols, int astride,
              const wg_outputs &o, const int32_t *plan, int blocks, const Geo &g, hipStream_t st) {
@@ -725,7 +874,7 @@ int run(const wg_batch *b, const wg_params *p, const float *action, int32_t cols
     if (b->N == 0 || n_steps <= 0) return 0;
     if (action && (cols < 0 || astride < cols)) return fail(WG_EINVAL, "bad action stride");
     if (action && p->action_mode == 1 && !b->muscle_stride) return fail(WG_EINVAL, "discrete actions need muscle_stride");
-    if (action && (!b->muscle_lo || !b->muscle_hi)) return fail(WG_EINVAL, "actions need muscle_lo/hi");
+    if (action && !b->muscle_bounds) return fail(WG_EINVAL, "actions need muscle_bounds");
     if (b->ragged && (!plan || plan_blocks <= 0)) return fail(WG_EINVAL, "ragged batch needs a plan");
     wg_outputs out = o ? *o : wg_outputs{};
     if (out.obs && out.obs_stride <= 0) return fail(WG_EINVAL, "obs_stride must be > 0");
@@ -799,6 +948,19 @@ int wg_plan_ragged(const int32_t *mass_off, const int32_t *edge_off, const int32
         plan[++blocks] = w;
     }
     return blocks;
+}
+
+// diagnostic builds: copy n block stamp records (8 x u64 each) to host memory; -1 otherwise
+int wg_debug_stamps(unsigned long long *host, int n) {
+#ifdef WG_STAMPS
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), (size_t)n * 8 * sizeof(unsigned long long), 0,
+                            hipMemcpyDeviceToHost) != hipSuccess)
+        return WG_EHIP;
+    return 0;
+#else
+    (void)host; (void)n;
+    return WG_EINVAL;
+#endif
 }
 
 int wg_launch_geometry(const wg_batch *b, wg_launch_info *info) {

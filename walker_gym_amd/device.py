@@ -12,9 +12,6 @@ import torch
 from . import _lib
 from .layout import HostLayout
 
-_TORCH = {np.dtype(np.float32): torch.float32, np.dtype(np.int32): torch.int32,
-          np.dtype(np.uint8): torch.uint8}
-
 
 def _to_dev(a: np.ndarray, device) -> torch.Tensor:
     a = np.ascontiguousarray(a)
@@ -51,16 +48,11 @@ class DeviceBatch:
         self.vel = _to_dev(host.vel, dv)
         self.acc = _to_dev(host.acc, dv)
         self.mass = _to_dev(host.mass, dv)
-        self.edge_ij = _to_dev(host.edge_ij, dv)
-        self.edge_rest = _to_dev(host.edge_rest, dv)
-        self.edge_k = _to_dev(host.edge_k, dv)
-        self.edge_c = _to_dev(host.edge_c, dv)
-        self.edge_flags = _to_dev(host.edge_flags, dv) if host.edge_flags.any() else None
+        self.edges = _to_dev(host.edges, dv)
         self.inc = _to_dev(host.inc, dv) if host.E else None
         self.inc_off = _to_dev(host.inc_off, dv)
         self.muscle_x = _to_dev(host.muscle_x, dv)
-        self.muscle_lo = _to_dev(host.muscle_lo, dv)
-        self.muscle_hi = _to_dev(host.muscle_hi, dv)
+        self.muscle_bounds = _to_dev(host.muscle_bounds, dv)
         self.muscle_stride = _to_dev(host.muscle_stride, dv)
         self.steps = _to_dev(host.steps, dv)
         self.contact = torch.zeros(self.P, dtype=torch.uint8, device=dv) if contact else None
@@ -93,10 +85,9 @@ class DeviceBatch:
             mass_off=self._p(self.mass_off) if r else None, edge_off=self._p(self.edge_off) if r else None,
             muscle_off=self._p(self.muscle_off) if r else None,
             pos=self._p(self.pos), vel=self._p(self.vel), acc=self._p(self.acc), mass=self._p(self.mass),
-            edge_ij=self._p(self.edge_ij), edge_rest=self._p(self.edge_rest), edge_k=self._p(self.edge_k),
-            edge_c=self._p(self.edge_c), edge_flags=self._p(self.edge_flags),
+            edges=self._p(self.edges),
             inc=self._p(self.inc) if self.inc is not None else None, inc_off=self._p(self.inc_off),
-            muscle_x=self._p(self.muscle_x), muscle_lo=self._p(self.muscle_lo), muscle_hi=self._p(self.muscle_hi),
+            muscle_x=self._p(self.muscle_x), muscle_bounds=self._p(self.muscle_bounds),
             muscle_stride=self._p(self.muscle_stride), steps=self._p(self.steps), contact=self._p(self.contact))
 
     def launch_geometry(self) -> dict:

@@ -1,0 +1,56 @@
+"""Multi-GPU data parallelism for the walker batch.
+
+Walkers are independent (no inter-walker force on the env path), so a node-wide batch shards into
+contiguous walker blocks, one per rank (one process per GPU, torch.distributed over RCCL/xGMI).
+Stepping needs no communication at all; the only collective is the observation gather at the end
+of a rollout (``gather_rollout``: one all_gather_into_tensor on RCCL, all_gather on gloo).
+Results of shard g are bit-identical to the same walkers stepped on one GPU (tested).
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+def shard_bounds(n_total: int, world: int, rank: int) -> Tuple[int, int]:
+    """Contiguous walker range [start, stop) of ``rank`` (the first n_total % world ranks get one more)."""
+    if world < 1 or not (0 <= rank < world):
+        raise ValueError("bad world/rank")
+    base, extra = divmod(n_total, world)
+    start = rank * base + min(rank, extra)
+    return start, start + base + (1 if rank < extra else 0)
+
+
+def shard_spec(spec: dict, start: int, stop: int) -> dict:
+    """Restrict a flat CSR walker spec to walkers [start, stop) (offsets rebased)."""
+    import numpy as np
+    mo, eo = np.asarray(spec["mass_off"]), np.asarray(spec["edge_off"])
+    nm = np.asarray(spec["n_muscles"])
+    uo = np.concatenate([[0], np.cumsum(nm)])
+    p0, p1, e0, e1, u0, u1 = mo[start], mo[stop], eo[start], eo[stop], uo[start], uo[stop]
+    out = {}
+    for k in ("m", "pos", "vel", "acc"):
+        if k in spec:
+            out[k] = np.asarray(spec[k])[p0:p1]
+    for k in ("ei", "ej", "rest", "k", "c", "flags"):
+        out[k] = np.asarray(spec[k])[e0:e1]
+    for k in ("minl", "maxl", "stride", "mx"):
+        if k in spec:
+            out[k] = np.asarray(spec[k])[u0:u1]
+    out["mass_off"] = (mo[start:stop + 1] - p0).astype(np.int32)
+    out["edge_off"] = (eo[start:stop + 1] - e0).astype(np.int32)
+    out["n_muscles"] = nm[start:stop].astype(np.int32)
+    return out
+
+
+def gather_rollout(local: torch.Tensor, group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:
+    """Concatenate every rank's [n, ...] block along dim 0 (equal n per rank) — the rollout-end gather."""
+    world = dist.get_world_size(group)
+    out = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    if dist.get_backend(group) == "nccl":
+        dist.all_gather_into_tensor(out, local.contiguous(), group=group)
+    else:
+        dist.all_gather(list(out.chunk(world, 0)), local.contiguous(), group=group)
+    return out

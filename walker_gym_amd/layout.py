@@ -5,10 +5,11 @@ The reference keeps one Python object per mass (gym/engine.py:24-59) and per edg
 ordered by walker so that any contiguous walker range is a contiguous byte range of every array:
 
   per mass   pos, vel, acc (old_a)  f32[P,3];  mass f32[P];  contact u8[P]
-  per edge   edge_ij u32[E] (i | j<<16, walker-local);  rest, k, c f32[E];  flags u8[E]
+  per edge   edges: 16-B records {ij = i | j<<16 | string<<31 (walker-local), rest, k, c} [E]
   per walker-edge-end   inc u16[2E] = (edge<<1 | end) sorted by (mass, edge, end);
              inc_off u16[P+N] (M_w+1 offsets per walker) — the deterministic accumulation order
-  per muscle muscle_x, lo = f32(originx*minl), hi = f32(originx*maxl), stride  f32[U]
+  per muscle muscle_x f32[U]; bounds (lo, hi) = (f32(originx*minl), f32(originx*maxl)) f32[U,2];
+             stride f32[U] (discrete actions)
   per walker steps i32[N]
 Muscles are the first A_w edges of each walker (Creature.run order, gym/optimized_walker.py:124-127).
 Uniform batches (one M/K/A) carry no offsets; ragged ones carry CSR mass_off/edge_off/muscle_off.
@@ -40,16 +41,11 @@ class HostLayout:
     vel: np.ndarray
     acc: np.ndarray
     mass: np.ndarray
-    edge_ij: np.ndarray
-    edge_rest: np.ndarray
-    edge_k: np.ndarray
-    edge_c: np.ndarray
-    edge_flags: np.ndarray
+    edges: np.ndarray          # uint32 [E, 4]: ij (with string bit 31), rest, k, c (float bits)
     inc: np.ndarray
     inc_off: np.ndarray
     muscle_x: np.ndarray
-    muscle_lo: np.ndarray
-    muscle_hi: np.ndarray
+    muscle_bounds: np.ndarray  # float32 [U, 2]
     muscle_stride: np.ndarray
     steps: np.ndarray
     extra: Dict[str, np.ndarray] = field(default_factory=dict)
@@ -135,7 +131,11 @@ def pack(spec: Dict[str, np.ndarray], mx: Optional[np.ndarray] = None, steps: Op
     ragged = not (np.all(Ms == Ms[0]) and np.all(Ks == Ks[0]) and np.all(n_mus == n_mus[0]))
     ei = np.ascontiguousarray(s["ei"], np.int64)
     ej = np.ascontiguousarray(s["ej"], np.int64)
-    edge_ij = (ei.astype(np.uint32) | (ej.astype(np.uint32) << np.uint32(16))).astype(np.uint32)
+    if Ms.max() > 32767:
+        raise ValueError("walker-local mass index does not fit the 15-bit edge endpoint encoding")
+    flags = np.ascontiguousarray(s["flags"], np.uint8)
+    edge_ij = (ei.astype(np.uint32) | (ej.astype(np.uint32) << np.uint32(16))
+               | ((flags & 1).astype(np.uint32) << np.uint32(31))).astype(np.uint32)
     inc, inc_off = incidence(ei, ej, mass_off, edge_off)
     rest = np.ascontiguousarray(s["rest"], f32)
     # muscle u of walker w is edge edge_off[w] + (u - muscle_off[w]); originx = its rest
@@ -149,16 +149,19 @@ def pack(spec: Dict[str, np.ndarray], mx: Optional[np.ndarray] = None, steps: Op
     hi = (x0 * maxl).astype(f32)
     pos = np.ascontiguousarray(s["pos"], f32).reshape(-1, 3)
     acc = spec.get("acc")
+    edges = np.stack([edge_ij, rest.view(np.uint32), np.ascontiguousarray(s["k"], f32).view(np.uint32),
+                      np.ascontiguousarray(s["c"], f32).view(np.uint32)], axis=1) if len(rest) else \
+        np.zeros((0, 4), np.uint32)
     return HostLayout(
         N=N, M=int(Ms.max()), K=int(Ks.max()), A=int(n_mus.max()), ragged=bool(ragged),
         mass_off=mass_off, edge_off=edge_off, muscle_off=muscle_off,
         pos=pos.copy(), vel=np.ascontiguousarray(s["vel"], f32).reshape(-1, 3).copy(),
         acc=(np.zeros_like(pos) if acc is None else np.ascontiguousarray(acc, f32).reshape(-1, 3).copy()),
-        mass=np.ascontiguousarray(s["m"], f32), edge_ij=edge_ij, edge_rest=rest,
-        edge_k=np.ascontiguousarray(s["k"], f32), edge_c=np.ascontiguousarray(s["c"], f32),
-        edge_flags=np.ascontiguousarray(s["flags"], np.uint8), inc=inc, inc_off=inc_off,
+        mass=np.ascontiguousarray(s["m"], f32), edges=np.ascontiguousarray(edges, np.uint32),
+        inc=inc, inc_off=inc_off,
         muscle_x=(x0.copy() if mx is None else np.ascontiguousarray(mx, f32).copy()),
-        muscle_lo=lo, muscle_hi=hi, muscle_stride=np.ascontiguousarray(s["stride"], f32),
+        muscle_bounds=np.ascontiguousarray(np.stack([lo, hi], axis=1).reshape(-1, 2), f32),
+        muscle_stride=np.ascontiguousarray(s["stride"], f32),
         steps=(np.zeros(N, np.int32) if steps is None else np.ascontiguousarray(steps, np.int32).copy()),
     )
 

@@ -1,0 +1,26 @@
+#!/usr/bin/env python3
+"""Average per-dispatch PMC values of the step kernel from gpurun_out/<tag>N/pmc_counter_collection.csv."""
+import collections
+import csv
+import glob
+import json
+import sys
+
+tag = sys.argv[1] if len(sys.argv) > 1 else "pmc"
+agg = collections.defaultdict(list)
+for f in sorted(glob.glob(f"gpurun_out/{tag}[0-9]*/pmc_counter_collection.csv")):
+    for r in csv.DictReader(open(f)):
+        if "walker_step_kernel" in r["Kernel_Name"]:
+            agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+out = {k: sum(v) / len(v) for k, v in agg.items()}
+for k, v in sorted(out.items()):
+    print(f"{k:24s} {v:16.1f}")
+if "SQ_WAVE_CYCLES" in out:
+    wc = out["SQ_WAVE_CYCLES"]
+    for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU"):
+        if k in out:
+            print(f"  {k}/WAVE_CYCLES = {out[k] / wc:.3f}")
+if "FETCH_SIZE" in out and "WRITE_SIZE" in out:
+    # gfx950: FETCH_SIZE reads half the bytes of wide coalesced streaming reads (MI355X_MICROARCH.md §HBM)
+    print(f"  HBM bytes/launch (2*FETCH + WRITE, KB->B): {(2 * out['FETCH_SIZE'] + out['WRITE_SIZE']) * 1024:.4g}")
+json.dump(out, open(f"gpurun_out/{tag}_summary.json", "w"), indent=1)

@@ -26,6 +26,7 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "walker_hip.h"
@@ -49,7 +50,8 @@ constexpr int EPL = 4;               // edges per lane per pass held in register
 #ifndef WG_NTHREADS
 #define WG_NTHREADS 256
 #endif
-constexpr int NTHREADS = WG_NTHREADS;
+constexpr int NTHREADS = WG_NTHREADS;   // default workgroup size (walkers fill 256 mass lanes)
+constexpr int MAXT = 256;               // __launch_bounds__: workgroups are 64..256 threads
 #ifndef WG_ABLATE
 #define WG_ABLATE 0   // profiling builds only (scripts/ablate.py): bit k skips phase k; 0 in the product
 #endif
@@ -214,22 +216,22 @@ __device__ inline double ddiv_exact(double a, double b, double y) {
 
 // Global -> LDS copy of n 4-byte words (16-B vector loads when both ends allow it).
 template <typename T4, typename T1>
-__device__ inline void stage_in(T1 *dst, const T1 *__restrict__ src, int n, int tid) {
+__device__ inline void stage_in(T1 *dst, const T1 *__restrict__ src, int n, int tid, int T) {
     if ((((uintptr_t)src) & 15) == 0 && (n & 3) == 0) {
         const T4 *s4 = reinterpret_cast<const T4 *>(src);
         T4 *d4 = reinterpret_cast<T4 *>(dst);
-        for (int i = tid; i < (n >> 2); i += NTHREADS) d4[i] = s4[i];
+        for (int i = tid; i < (n >> 2); i += T) d4[i] = s4[i];
     } else {
-        for (int i = tid; i < n; i += NTHREADS) dst[i] = src[i];
+        for (int i = tid; i < n; i += T) dst[i] = src[i];
     }
 }
-__device__ inline void stage_out(float *__restrict__ dst, const float *src, int n, int tid) {
+__device__ inline void stage_out(float *__restrict__ dst, const float *src, int n, int tid, int T) {
     if ((((uintptr_t)dst) & 15) == 0 && (n & 3) == 0) {
         const float4 *s4 = reinterpret_cast<const float4 *>(src);
         float4 *d4 = reinterpret_cast<float4 *>(dst);
-        for (int i = tid; i < (n >> 2); i += NTHREADS) d4[i] = s4[i];
+        for (int i = tid; i < (n >> 2); i += T) d4[i] = s4[i];
     } else {
-        for (int i = tid; i < n; i += NTHREADS) dst[i] = src[i];
+        for (int i = tid; i < n; i += T) dst[i] = src[i];
     }
 }
 
@@ -242,6 +244,107 @@ __device__ inline EdgeRec load_edge(const wg_edge *__restrict__ e, size_t i) {
 __device__ inline int edge_i(uint32_t ij) { return (int)(ij & 0x7fffu); }
 __device__ inline int edge_j(uint32_t ij) { return (int)((ij >> 16) & 0x7fffu); }
 __device__ inline bool edge_string(uint32_t ij) { return (ij >> 31) != 0u; }
+
+// ------------------------------------------------------------------ per-edge and per-mass physics
+// Spring term and damping force of edge `le` (block-local; masses at LDS index lm + i/j):
+//   spring  gym/engine.py:78-102 resilience (two anti_forced calls, float64 force path, :73-75)
+//   damping gym/optimized_walker.py:92-106 (float32), the same expression for every element type
+// spring_mode 1 = the G2 element as written (gym/optimized_walker.py:48-60: float32, inverted sign).
+__device__ __forceinline__ void spring_edge(const EdgeRec &e, int le, int lm, float x, const float *spos,
+                                            const float *svel, double *st, float *sdf, int spring_mode) {
+    const int i = lm + edge_i(e.ij), j = lm + edge_j(e.ij);
+    const float pix = spos[3 * i], piy = spos[3 * i + 1], piz = spos[3 * i + 2];
+    const float pjx = spos[3 * j], pjy = spos[3 * j + 1], pjz = spos[3 * j + 2];
+    const float vix = svel[3 * i], viy = svel[3 * i + 1], viz = svel[3 * i + 2];
+    const float vjx = svel[3 * j], vjy = svel[3 * j + 1], vjz = svel[3 * j + 2];
+    const float cur = np_norm3(pix - pjx, piy - pjy, piz - pjz);   // engine.py:86
+    const float dx = cur - x;                                       // engine.py:96
+    const float r0 = pjx - pix, r1 = pjy - piy, r2 = pjz - piz;     // other.pos - self.pos
+    double dist = (double)cur;                                      // engine.py:73
+    if (CONFIG_R > dist) dist = CONFIG_R;                           // max(distance, r)
+    const double yc = 1.0 / dist;
+    float d0 = r0, d1 = r1, d2 = r2;
+    if (cur > 0.f) {                                                // optimized_walker.py:93
+        if ((double)cur == dist) {
+            const float ycf = (float)yc;
+            d0 = fdiv_mk(r0, cur, ycf); d1 = fdiv_mk(r1, cur, ycf); d2 = fdiv_mk(r2, cur, ycf);
+        } else {
+            d0 = r0 / cur; d1 = r1 / cur; d2 = r2 / cur;
+        }
+    }
+    double t0, t1, t2;
+    if (spring_mode == 1) {
+        const float fs = (-dx) * e.k;
+        t0 = (double)(fs * d0); t1 = (double)(fs * d1); t2 = (double)(fs * d2);
+    } else {
+        const float fsz = (dx < 0.f && edge_string(e.ij)) ? 0.f : (-dx) * e.k;   // engine.py:97-100
+        const float nf = -fsz;                                                    // engine.py:75
+        t0 = ddiv_exact((double)(nf * r0), dist, yc);
+        t1 = ddiv_exact((double)(nf * r1), dist, yc);
+        t2 = ddiv_exact((double)(nf * r2), dist, yc);
+    }
+    st[3 * le] = t0; st[3 * le + 1] = t1; st[3 * le + 2] = t2;
+    const float dk = np_dot3(vix - vjx, viy - vjy, viz - vjz, d0, d1, d2);  // :102-103
+    const float dkc = dk * e.c;                                               // :104
+    sdf[3 * le] = dkc * d0; sdf[3 * le + 1] = dkc * d1; sdf[3 * le + 2] = dkc * d2;
+}
+
+// Mass `lp`: the ordered force accumulation over its incidence list (edge order, spring then damping
+// per edge — gym/optimized_walker.py:124-127 with gym/engine.py:65-76, 101-102), then gravity, linear
+// damping and the ground penalty (gym/env.py:31-41 / gym/optimized_env.py:146-172, each one
+// Point.forced), then Point.run1 (gym/engine.py:174-178).  Returns the new state and old_a.
+__device__ __forceinline__ void mass_step(const KParams &kp, const double *st, const float *sdf,
+                                          const uint16_t *inc, int lb, int s0, int s1, float mf,
+                                          const float *p3, const float *v3, float &px, float &py, float &pz,
+                                          float &vx, float &vy, float &vz, float &ax, float &ay, float &az,
+                                          bool &hit) {
+    const double md = (double)mf;
+    const double ym = 1.0 / md;      // one IEEE division per mass; every /m below is exact from it
+    const float ymf = (float)ym;     // = RN32(1/m)
+    ax = 0.f; ay = 0.f; az = 0.f;
+    for (int r = s0; r < s1; r++) {
+        const int ent = inc[r];
+        const int le = lb + (ent >> 1);
+        const bool end_j = ent & 1;
+        const double t0 = st[3 * le], t1 = st[3 * le + 1], t2 = st[3 * le + 2];
+        const float f0 = sdf[3 * le], f1 = sdf[3 * le + 1], f2 = sdf[3 * le + 2];
+        if (kp.spring_mode == 1) {
+            const float sg = end_j ? -1.f : 1.f;
+            ax = ax + fdiv_mk(sg * (float)t0, mf, ymf);
+            ay = ay + fdiv_mk(sg * (float)t1, mf, ymf);
+            az = az + fdiv_mk(sg * (float)t2, mf, ymf);
+        } else {
+            // Point.forced with a float64 force: a = f32(f64(a) + t/m)   (engine.py:67,75)
+            const double sg = end_j ? -1.0 : 1.0;
+            ax = (float)((double)ax + ddiv_exact(sg * t0, md, ym));
+            ay = (float)((double)ay + ddiv_exact(sg * t1, md, ym));
+            az = (float)((double)az + ddiv_exact(sg * t2, md, ym));
+        }
+        // damping: p1.forced(-damp_force); p2.forced(damp_force)  (optimized_walker.py:105-106)
+        const float sf = end_j ? 1.f : -1.f;
+        ax = ax + fdiv_mk(sf * f0, mf, ymf);
+        ay = ay + fdiv_mk(sf * f1, mf, ymf);
+        az = az + fdiv_mk(sf * f2, mf, ymf);
+    }
+    vx = v3[0]; vy = v3[1]; vz = v3[2];
+    px = p3[0]; py = p3[1]; pz = p3[2];
+    const float zm = fdiv_mk(0.f, mf, ymf);   // the zero components of the env forces, divided by m
+    // gravity [0,-g,0]/m, damp -dampk*v/m  (gym/env.py:32-33, optimized_env.py:148-151)
+    ax = ax + zm; ay = ay + fdiv_mk(kp.neg_g, mf, ymf); az = az + zm;
+    ax = ax + fdiv_mk(kp.neg_dampk * vx, mf, ymf);
+    ay = ay + fdiv_mk(kp.neg_dampk * vy, mf, ymf);
+    az = az + fdiv_mk(kp.neg_dampk * vz, mf, ymf);
+    const float deep = py - kp.ground;
+    hit = deep < 0.f;                                                // optimized_env.py:154
+    if (hit) {
+        ax = ax + zm; ay = ay + fdiv_mk(kp.neg_groundk * deep, mf, ymf); az = az + zm;
+        ax = ax + zm; ay = ay + fdiv_mk(kp.neg_grounddamp * vy, mf, ymf); az = az + zm;
+        const float ff = fabsf(deep) * kp.friction;                  // :168
+        ax = ax + fdiv_mk((-vx) * ff, mf, ymf); ay = ay + zm; az = az + fdiv_mk((-vz) * ff, mf, ymf);
+    }
+    vx = vx + ax * kp.dt; vy = vy + ay * kp.dt; vz = vz + az * kp.dt;   // Point.run1
+    px = px + vx * kp.dt; py = py + vy * kp.dt; pz = pz + vz * kp.dt;
+}
 
 // ------------------------------------------------------------------ cross-lane reductions
 // A walker's M masses are M adjacent lanes of one wave when M divides 64 (uniform batches): numpy's
@@ -273,12 +376,12 @@ __device__ inline float pw_sum_lanes(float x, int base, int M, int lane) {
 // STEP = false: observe only (reset path).  RAGGED: CSR offsets + block plan.  IN3D: obs layout.
 // PWD: pairwise-sum recursion depth (0: M <= 128).  SHFL: register reductions (uniform, M | 64).
 template <bool STEP, bool RAGGED, bool IN3D, int PWD, bool SHFL>
-__global__ __launch_bounds__(NTHREADS) void walker_step_kernel(
+__global__ __launch_bounds__(MAXT) void walker_step_kernel(
     wg_batch b, KParams kp, const float *__restrict__ action, int action_cols, int action_stride,
     wg_outputs o, const int32_t *__restrict__ plan, Geo geo) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     Carve s = carve(smem, geo);
-    const int tid = threadIdx.x, lane = tid & 63;
+    const int tid = threadIdx.x, lane = tid & 63, T = blockDim.x;
     STAMP(0);
 
     // ---- this workgroup's walker range and flat slices
@@ -291,7 +394,7 @@ __global__ __launch_bounds__(NTHREADS) void walker_step_kernel(
         P0 = b.mass_off[w0]; P1 = b.mass_off[w1];
         E0 = b.edge_off[w0]; E1 = b.edge_off[w1];
         U0 = b.muscle_off[w0]; U1 = b.muscle_off[w1];
-        for (int i = tid; i <= nw; i += NTHREADS) {
+        for (int i = tid; i <= nw; i += T) {
             s.moff[i] = b.mass_off[w0 + i] - P0;
             s.eoff[i] = b.edge_off[w0 + i] - E0;
             s.uoff[i] = b.muscle_off[w0 + i] - U0;
@@ -302,19 +405,19 @@ __global__ __launch_bounds__(NTHREADS) void walker_step_kernel(
     const int nP = P1 - P0, nE = E1 - E0, nU = U1 - U0;
 
     // ================= phase 0: issue every global load of the tile =================
-    stage_in<float4>(s.pos, b.pos + 3 * (size_t)P0, 3 * nP, tid);
-    stage_in<float4>(s.vel, b.vel + 3 * (size_t)P0, 3 * nP, tid);
-    if (!STEP && !SHFL) stage_in<float4>(s.acc, b.acc + 3 * (size_t)P0, 3 * nP, tid);
-    if (!SHFL) stage_in<float4>(s.m, b.mass + P0, nP, tid);
+    stage_in<float4>(s.pos, b.pos + 3 * (size_t)P0, 3 * nP, tid, T);
+    stage_in<float4>(s.vel, b.vel + 3 * (size_t)P0, 3 * nP, tid, T);
+    if (!STEP && !SHFL) stage_in<float4>(s.acc, b.acc + 3 * (size_t)P0, 3 * nP, tid, T);
+    if (!SHFL) stage_in<float4>(s.m, b.mass + P0, nP, tid, T);
     if (STEP && nE > 0)
-        stage_in<uint4>(s.inc, reinterpret_cast<const uint32_t *>(b.inc) + E0, nE, tid);
+        stage_in<uint4>(s.inc, reinterpret_cast<const uint32_t *>(b.inc) + E0, nE, tid, T);
 
     // edge records of this lane's first pass -> registers
     EdgeRec er[EPL];
     if (STEP) {
 #pragma unroll
         for (int it = 0; it < EPL; it++) {
-            const int le = tid + it * NTHREADS;
+            const int le = tid + it * T;
             if (le < nE) er[it] = load_edge(b.edges, E0 + le);
         }
     }
@@ -357,7 +460,7 @@ __global__ __launch_bounds__(NTHREADS) void walker_step_kernel(
 
     // ================= 1. act: Creature.act -> Muscle.act / actdisp -> regulation =================
     // (gym/optimized_walker.py:27-43,164-172)
-    for (int u = tid; u < nU; u += NTHREADS) {
+    for (int u = tid; u < nU; u += T) {
         const bool first = (u == tid);
         float x = first ? mu_x : b.muscle_x[U0 + u];
         if (STEP && action) {
@@ -393,10 +496,10 @@ __global__ __launch_bounds__(NTHREADS) void walker_step_kernel(
     if (STEP) {
         // ================= 2. edge phase =================
         // spring (gym/engine.py:78-102) + damping (gym/optimized_walker.py:92-106)
-        for (int pass = 0; pass * EPL * NTHREADS < nE; pass++) {
+        for (int pass = 0; pass * EPL * T < nE; pass++) {
 #pragma unroll
             for (int it = 0; it < EPL; it++) {
-                const int le = tid + (pass * EPL + it) * NTHREADS;
+                const int le = tid + (pass * EPL + it) * T;
                 if (le >= nE) break;
                 const EdgeRec e = (pass == 0) ? er[it] : load_edge(b.edges, E0 + le);
                 if (WG_ABLATE & 1) {
@@ -412,43 +515,7 @@ __global__ __launch_bounds__(NTHREADS) void walker_step_kernel(
                     const int wl = fdiv(le, b.K, geo.invK);
                     lm = wl * b.M; ew = le - wl * b.K; Aw = b.A; ub = wl * b.A;
                 }
-                const int i = lm + edge_i(e.ij), j = lm + edge_j(e.ij);
-                const float x = (ew < Aw) ? s.x[ub + ew] : e.rest;
-                const float pix = s.pos[3 * i], piy = s.pos[3 * i + 1], piz = s.pos[3 * i + 2];
-                const float pjx = s.pos[3 * j], pjy = s.pos[3 * j + 1], pjz = s.pos[3 * j + 2];
-                const float vix = s.vel[3 * i], viy = s.vel[3 * i + 1], viz = s.vel[3 * i + 2];
-                const float vjx = s.vel[3 * j], vjy = s.vel[3 * j + 1], vjz = s.vel[3 * j + 2];
-                const float cur = np_norm3(pix - pjx, piy - pjy, piz - pjz);   // engine.py:86
-                const float dx = cur - x;                                       // engine.py:96
-                const float r0 = pjx - pix, r1 = pjy - piy, r2 = pjz - piz;     // other.pos - self.pos
-                double dist = (double)cur;                                      // engine.py:73
-                if (CONFIG_R > dist) dist = CONFIG_R;                           // max(distance, r)
-                const double yc = 1.0 / dist;
-                float d0 = r0, d1 = r1, d2 = r2;
-                if (cur > 0.f) {                                                // optimized_walker.py:93
-                    if ((double)cur == dist) {
-                        const float ycf = (float)yc;
-                        d0 = fdiv_mk(r0, cur, ycf); d1 = fdiv_mk(r1, cur, ycf); d2 = fdiv_mk(r2, cur, ycf);
-                    } else {
-                        d0 = r0 / cur; d1 = r1 / cur; d2 = r2 / cur;
-                    }
-                }
-                double t0, t1, t2;
-                if (kp.spring_mode == 1) {
-                    // G2 element (gym/optimized_walker.py:48-60): float32 force, inverted sign.
-                    const float fs = (-dx) * e.k;
-                    t0 = (double)(fs * d0); t1 = (double)(fs * d1); t2 = (double)(fs * d2);
-                } else {
-                    const float fsz = (dx < 0.f && edge_string(e.ij)) ? 0.f : (-dx) * e.k;   // engine.py:97-100
-                    const float nf = -fsz;                                                    // engine.py:75
-                    t0 = ddiv_exact((double)(nf * r0), dist, yc);
-                    t1 = ddiv_exact((double)(nf * r1), dist, yc);
-                    t2 = ddiv_exact((double)(nf * r2), dist, yc);
-                }
-                s.t[3 * le] = t0; s.t[3 * le + 1] = t1; s.t[3 * le + 2] = t2;
-                const float dk = np_dot3(vix - vjx, viy - vjy, viz - vjz, d0, d1, d2);  // :102-103
-                const float dkc = dk * e.c;                                               // :104
-                s.df[3 * le] = dkc * d0; s.df[3 * le + 1] = dkc * d1; s.df[3 * le + 2] = dkc * d2;
+                spring_edge(e, le, lm, (ew < Aw) ? s.x[ub + ew] : e.rest, s.pos, s.vel, s.t, s.df, kp.spring_mode);
             }
         }
         __syncthreads();
@@ -456,7 +523,7 @@ __global__ __launch_bounds__(NTHREADS) void walker_step_kernel(
 
         // ================= 3. mass phase: ordered accumulation, env forces, run1 =================
         const uint16_t *s_inc16 = reinterpret_cast<const uint16_t *>(s.inc);
-        for (int lp = tid; lp < nP; lp += NTHREADS) {
+        for (int lp = tid; lp < nP; lp += T) {
             const bool first = (lp == tid);
             int wl, lm;
             if (first) { wl = my_wl; lm = my_lm; }
@@ -470,53 +537,10 @@ __global__ __launch_bounds__(NTHREADS) void walker_step_kernel(
             }
             const float mf = SHFL ? my_m : s.m[lp];
             const double md = (double)mf;
-            const double ym = 1.0 / md;      // one IEEE division per mass; every /m below is exact from it
-            const float ymf = (float)ym;     // = RN32(1/m)
-            ax = 0.f; ay = 0.f; az = 0.f;
-            for (int r = s0; r < ((WG_ABLATE & 2) ? s0 + 1 : s1); r++) {
-                const int ent = s_inc16[2 * lb + r];
-                const int le = lb + (ent >> 1);
-                const bool end_j = ent & 1;
-                const double t0 = s.t[3 * le], t1 = s.t[3 * le + 1], t2 = s.t[3 * le + 2];
-                const float f0 = s.df[3 * le], f1 = s.df[3 * le + 1], f2 = s.df[3 * le + 2];
-                if (kp.spring_mode == 1) {
-                    const float sg = end_j ? -1.f : 1.f;
-                    ax = ax + fdiv_mk(sg * (float)t0, mf, ymf);
-                    ay = ay + fdiv_mk(sg * (float)t1, mf, ymf);
-                    az = az + fdiv_mk(sg * (float)t2, mf, ymf);
-                } else {
-                    // Point.forced with a float64 force: a = f32(f64(a) + t/m)   (engine.py:67,75)
-                    const double sg = end_j ? -1.0 : 1.0;
-                    ax = (float)((double)ax + ddiv_exact(sg * t0, md, ym));
-                    ay = (float)((double)ay + ddiv_exact(sg * t1, md, ym));
-                    az = (float)((double)az + ddiv_exact(sg * t2, md, ym));
-                }
-                // damping: p1.forced(-damp_force); p2.forced(damp_force)  (optimized_walker.py:105-106)
-                const float sf = end_j ? 1.f : -1.f;
-                ax = ax + fdiv_mk(sf * f0, mf, ymf);
-                ay = ay + fdiv_mk(sf * f1, mf, ymf);
-                az = az + fdiv_mk(sf * f2, mf, ymf);
-            }
-            vx = s.vel[3 * lp]; vy = s.vel[3 * lp + 1]; vz = s.vel[3 * lp + 2];
-            px = s.pos[3 * lp]; py = s.pos[3 * lp + 1]; pz = s.pos[3 * lp + 2];
-            const float zm = fdiv_mk(0.f, mf, ymf);   // the zero components of the env forces, divided by m
-            // gravity [0,-g,0]/m, damp -dampk*v/m  (gym/env.py:32-33, optimized_env.py:148-151)
-            ax = ax + zm; ay = ay + fdiv_mk(kp.neg_g, mf, ymf); az = az + zm;
-            ax = ax + fdiv_mk(kp.neg_dampk * vx, mf, ymf);
-            ay = ay + fdiv_mk(kp.neg_dampk * vy, mf, ymf);
-            az = az + fdiv_mk(kp.neg_dampk * vz, mf, ymf);
-            const float deep = py - kp.ground;
-            const bool hit = deep < 0.f;                                     // optimized_env.py:154
-            if (hit) {
-                ax = ax + zm; ay = ay + fdiv_mk(kp.neg_groundk * deep, mf, ymf); az = az + zm;
-                ax = ax + zm; ay = ay + fdiv_mk(kp.neg_grounddamp * vy, mf, ymf); az = az + zm;
-                const float ff = fabsf(deep) * kp.friction;                   // :168
-                ax = ax + fdiv_mk((-vx) * ff, mf, ymf); ay = ay + zm; az = az + fdiv_mk((-vz) * ff, mf, ymf);
-            }
+            bool hit;
+            mass_step(kp, s.t, s.df, s_inc16 + 2 * lb, lb, s0, (WG_ABLATE & 2) ? min(s1, s0 + 1) : s1, mf,
+                      s.pos + 3 * lp, s.vel + 3 * lp, px, py, pz, vx, vy, vz, ax, ay, az, hit);
             if (b.contact) b.contact[P0 + lp] = (uint8_t)hit;
-            // Point.run1 (gym/engine.py:174-178)
-            vx = vx + ax * kp.dt; vy = vy + ay * kp.dt; vz = vz + az * kp.dt;
-            px = px + vx * kp.dt; py = py + vy * kp.dt; pz = pz + vz * kp.dt;
             s.pos[3 * lp] = px; s.pos[3 * lp + 1] = py; s.pos[3 * lp + 2] = pz;
             s.vel[3 * lp] = vx; s.vel[3 * lp + 1] = vy; s.vel[3 * lp + 2] = vz;
             if (SHFL) {      // old_a straight from registers (no LDS copy in the register-reduction kernel)
@@ -532,7 +556,7 @@ __global__ __launch_bounds__(NTHREADS) void walker_step_kernel(
             if (!SHFL) { s.nrm[lp] = nv; s.ke[lp] = ke; s.pe[lp] = pe; }
         }
     } else {
-        for (int lp = tid; lp < nP; lp += NTHREADS) {
+        for (int lp = tid; lp < nP; lp += T) {
             const float mf = SHFL ? my_m : s.m[lp];
             vx = s.vel[3 * lp]; vy = s.vel[3 * lp + 1]; vz = s.vel[3 * lp + 2];
             px = s.pos[3 * lp]; py = s.pos[3 * lp + 1]; pz = s.pos[3 * lp + 2];
@@ -591,15 +615,15 @@ __global__ __launch_bounds__(NTHREADS) void walker_step_kernel(
     STAMP(3);
 
     if (STEP) {
-        stage_out(b.pos + 3 * (size_t)P0, s.pos, 3 * nP, tid);
-        stage_out(b.vel + 3 * (size_t)P0, s.vel, 3 * nP, tid);
-        if (!SHFL) stage_out(b.acc + 3 * (size_t)P0, s.acc, 3 * nP, tid);
+        stage_out(b.pos + 3 * (size_t)P0, s.pos, 3 * nP, tid, T);
+        stage_out(b.vel + 3 * (size_t)P0, s.vel, 3 * nP, tid, T);
+        if (!SHFL) stage_out(b.acc + 3 * (size_t)P0, s.acc, 3 * nP, tid, T);
     }
     if (!SHFL) {
         // 8 lanes per walker, numpy's summation orders (see oracle/walker_oracle.c walker_observe):
         // r 0-2 sequential sums of pos[:, r] (getstat mid / info centroid), r 3 pairwise sum of y
         // (np.mean), r 4-6 pairwise sums of |v|, m|v|^2, m*g*(y-ground), r 7 contact count + all-stopped.
-        for (int idx = tid; idx < ((WG_ABLATE & 8) ? 0 : nw * 8); idx += NTHREADS) {
+        for (int idx = tid; idx < ((WG_ABLATE & 8) ? 0 : nw * 8); idx += T) {
             const int wl = idx >> 3, r = idx & 7;
             const int lm = RAGGED ? s.moff[wl] : wl * b.M;
             const int M = RAGGED ? s.moff[wl + 1] - lm : b.M;
@@ -687,7 +711,7 @@ __global__ __launch_bounds__(NTHREADS) void walker_step_kernel(
             }
         } else {
             // per-mass block of 3*d values: (pos - mid)*pk, v*vk, old_a*ak
-            for (int lp = tid; lp < nP; lp += NTHREADS) {
+            for (int lp = tid; lp < nP; lp += T) {
                 int wl, lm;
                 if (lp == tid) { wl = my_wl; lm = my_lm; }
                 else if (RAGGED) { wl = locate(s.moff, nw, lp); lm = s.moff[wl]; }
@@ -704,7 +728,7 @@ __global__ __launch_bounds__(NTHREADS) void walker_step_kernel(
                 }
             }
             // conmid columns and zero padding of short (ragged) rows
-            for (int wl = tid; wl < nw; wl += NTHREADS) {
+            for (int wl = tid; wl < nw; wl += T) {
                 const int lm = RAGGED ? s.moff[wl] : wl * b.M;
                 const int M = RAGGED ? s.moff[wl + 1] - lm : b.M;
                 const int A = RAGGED ? s.uoff[wl + 1] - s.uoff[wl] : b.A;
@@ -715,7 +739,7 @@ __global__ __launch_bounds__(NTHREADS) void walker_step_kernel(
             }
         }
         // muscle rest lengths x*mk
-        for (int u = tid; u < nU; u += NTHREADS) {
+        for (int u = tid; u < nU; u += T) {
             int wl, ua, M;
             if (RAGGED) { wl = locate(s.uoff, nw, u); ua = u - s.uoff[wl]; M = s.moff[wl + 1] - s.moff[wl]; }
             else { wl = fdiv(u, b.A, geo.invA); ua = u - wl * b.A; M = b.M; }
@@ -724,10 +748,189 @@ __global__ __launch_bounds__(NTHREADS) void walker_step_kernel(
         if (!RAGGED) {
             __syncthreads();
             STAMP(5);
-            stage_out(ob, tile, nw * stride, tid);
+            stage_out(ob, tile, nw * stride, tid, T);
         }
     }
     STAMP(6);
+}
+
+
+// ------------------------------------------------------------------ streaming (persistent) kernel
+// Uniform batches with register reductions (M | 64): persistent workgroups walk tiles of W walkers and
+// keep the NEXT tile's global loads (state, incidence, spring / muscle records) in flight in registers
+// while the current tile computes, so the chip does not alternate between an all-load phase and an
+// all-compute phase (measured phase lock of the one-tile-per-workgroup kernel).
+typedef float vf4 __attribute__((ext_vector_type(4)));   // native vectors keep loop-carried values in VGPRs
+typedef unsigned vu4 __attribute__((ext_vector_type(4)));
+typedef float vf2 __attribute__((ext_vector_type(2)));
+
+template <bool IN3D, int NE>
+__global__ __launch_bounds__(MAXT) void walker_step_stream(
+    wg_batch b, KParams kp, const float *__restrict__ action, int action_cols, int action_stride,
+    wg_outputs o, Geo geo, int ntiles) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const Carve s = carve(smem, geo);
+    const int tid = threadIdx.x, lane = tid & 63, T = blockDim.x;
+    const int W = geo.W, M = b.M, K = b.K, A = b.A;
+    const int nP = W * M, nE = W * K, nU = W * A;
+    // fixed lane roles
+    const bool is_mass = tid < nP, is_mus = tid < nU;
+    const int my_wl = fdiv(tid, M, geo.invM), my_q = tid - my_wl * M;
+    const int gbase = (tid & ~63) + ((lane / M) * M);            // first lane of my walker in this wave
+    const int mu_wl = A > 0 ? fdiv(tid, A, geo.invA) : 0, mu_ua = tid - mu_wl * A;
+    const bool acts = action != nullptr && is_mus && mu_ua < action_cols;
+    const int n3 = 3 * nP / 4, n1 = nP / 4, ni = nE / 4;
+    // clamped per-lane indices: every prefetch load is unconditional (no branches around loads)
+    const int i3 = min(tid, n3 - 1), i1 = min(tid, n1 - 1), ii = min(tid, max(ni - 1, 0));
+    const int iu = min(tid, max(nU - 1, 0)), iw = min(my_wl, W - 1), iq = min(my_q, M - 1);
+    const int iau = min(mu_ua, max(A - 1, 0)), iaw = min(mu_wl, W - 1);
+
+    vf4 pp, pv; vu4 pi = vu4{0u, 0u, 0u, 0u}; vu4 pe[NE];
+    float pm, pmx = 0.f, pact = 0.f, pst = 0.f; vf2 pbd = vf2{0.f, 0.f};
+    uint32_t pio = 0u; int psteps;
+#define WG_PREFETCH(tile_)                                                                                  \
+    do {                                                                                                    \
+        const int w0_ = (tile_) * W;                                                                        \
+        const size_t P0_ = (size_t)w0_ * M, E0_ = (size_t)w0_ * K, U0_ = (size_t)w0_ * A;                   \
+        pp = reinterpret_cast<const vf4 *>(b.pos + 3 * P0_)[i3];                                             \
+        pv = reinterpret_cast<const vf4 *>(b.vel + 3 * P0_)[i3];                                             \
+        pm = b.mass[P0_ + min(tid, nP - 1)];                                                                 \
+        if (nE > 0) {                                                                                        \
+            pi = reinterpret_cast<const vu4 *>(reinterpret_cast<const uint32_t *>(b.inc) + E0_)[ii];         \
+            _Pragma("unroll") for (int it = 0; it < NE; it++)                                                \
+                pe[it] = reinterpret_cast<const vu4 *>(b.edges)[E0_ + min(tid + it * T, nE - 1)];            \
+            const uint16_t *io_ = b.inc_off + P0_ + (size_t)w0_ + (size_t)iw * (M + 1) + iq;                 \
+            pio = (uint32_t)io_[0] | ((uint32_t)io_[1] << 16);                                               \
+        }                                                                                                    \
+        if (nU > 0) {                                                                                        \
+            pmx = b.muscle_x[U0_ + iu];                                                                      \
+            if (action) {                                                                                    \
+                pbd = reinterpret_cast<const vf2 *>(b.muscle_bounds)[U0_ + iu];                              \
+                if (kp.action_mode == 1) pst = b.muscle_stride[U0_ + iu];                                    \
+                pact = action[(size_t)(w0_ + iaw) * action_stride + iau];                                    \
+            }                                                                                                \
+        }                                                                                                    \
+        psteps = b.steps[w0_ + iw];                                                                          \
+    } while (0)
+
+    int tile = blockIdx.x;
+    if (tile < ntiles) WG_PREFETCH(tile);
+    for (; tile < ntiles; tile += gridDim.x) {
+        const int w0 = tile * W;
+        const size_t P0 = (size_t)w0 * M, U0 = (size_t)w0 * A;
+        // ---- commit the prefetched tile: state to LDS, records to this iteration's registers
+        if (tid < n3) { reinterpret_cast<vf4 *>(s.pos)[tid] = pp; reinterpret_cast<vf4 *>(s.vel)[tid] = pv; }
+        if (tid < ni) reinterpret_cast<vu4 *>(s.inc)[tid] = pi;
+        vu4 ce[NE];
+        _Pragma("unroll") for (int it = 0; it < NE; it++) ce[it] = pe[it];
+        const float mf = pm, bx = pmx, ba = pact, bst = pst;
+        const vf2 bd = pbd;
+        const uint32_t io = pio;
+        const int wsteps = psteps;
+        // ---- the next tile's loads go in flight now
+        if (tile + (int)gridDim.x < ntiles) WG_PREFETCH(tile + (int)gridDim.x);
+
+        // ---- act (gym/optimized_walker.py:27-43,164-172)
+        float x = bx;
+        if (acts) {
+            x = (kp.action_mode == 1) ? ((ba != 0.f) ? x + bst : x - bst) : x + ba;
+            if (bd.x > x) x = bd.x;     // Python max(x, originx*minl)
+            if (bd.y < x) x = bd.y;     // Python min(x, originx*maxl)
+            b.muscle_x[U0 + tid] = x;
+        }
+        if (is_mus) s.x[tid] = x;
+        __syncthreads();
+
+        // ---- edge phase
+        _Pragma("unroll") for (int it = 0; it < NE; it++) {
+            const int le = tid + it * T;
+            if (le < nE) {
+                const EdgeRec e{ce[it].x, __uint_as_float(ce[it].y), __uint_as_float(ce[it].z), __uint_as_float(ce[it].w)};
+                const int wl = fdiv(le, K, geo.invK), ew = le - wl * K;
+                spring_edge(e, le, wl * M, (ew < A) ? s.x[wl * A + ew] : e.rest, s.pos, s.vel, s.t, s.df, kp.spring_mode);
+            }
+        }
+        __syncthreads();
+
+        // ---- mass phase
+        float px = 0.f, py = 0.f, pz = 0.f, vx = 0.f, vy = 0.f, vz = 0.f, ax = 0.f, ay = 0.f, az = 0.f;
+        float nv = 0.f, ke = 0.f, pe_ = 0.f;
+        if (is_mass) {
+            bool hit;
+            const int lb = my_wl * K;
+            mass_step(kp, s.t, s.df, reinterpret_cast<const uint16_t *>(s.inc) + 2 * lb, lb, (int)(io & 0xffffu),
+                      (int)(io >> 16), mf, s.pos + 3 * tid, s.vel + 3 * tid, px, py, pz, vx, vy, vz, ax, ay, az, hit);
+            if (b.contact) b.contact[P0 + tid] = (uint8_t)hit;
+            float *ga = b.acc + 3 * (P0 + tid);
+            ga[0] = ax; ga[1] = ay; ga[2] = az;
+            nv = np_norm3(vx, vy, vz);
+            ke = mf * (nv * nv);     // numpy's float32 ** 2 is libm powf: may differ by 1 ulp
+            pe_ = (float)((double)mf * kp.g) * (py - kp.ground);
+        }
+        // per-walker reductions in registers (all lanes of the wave take part in the shuffles)
+        const float sx = seq_sum_lanes(px, gbase, M), sy = seq_sum_lanes(py, gbase, M), sz = seq_sum_lanes(pz, gbase, M);
+        const float ysum = pw_sum_lanes(py, gbase, M, lane), vsum = pw_sum_lanes(nv, gbase, M, lane);
+        const float ksum = pw_sum_lanes(ke, gbase, M, lane), psum = pw_sum_lanes(pe_, gbase, M, lane);
+        const unsigned long long gmask = (M == 64) ? ~0ull : (((1ull << M) - 1ull) << (gbase & 63));
+        const unsigned long long hb = __ballot(is_mass && (py - kp.ground < 0.f));   // contacts after run1 (:200)
+        const unsigned long long sb = __ballot(is_mass && nv < 0.1f);
+        const float fM = (float)M;
+        const float midx = sx / fM, midy = sy / fM, midz = sz / fM;
+        if (is_mass && my_q == 0) {                                   // gym/optimized_env.py:189-248
+            const size_t wg = (size_t)(w0 + my_wl);
+            const int steps = wsteps + 1;
+            b.steps[wg] = steps;
+            const float cy = ysum / fM;
+            if (o.reward) {
+                const float vpen = (-(vsum / fM)) * 0.1f;
+                o.reward[wg] = (cy + vpen) + (float)(-(double)__popcll(hb & gmask) * 0.5);
+            }
+            if (o.done) {
+                int done = steps >= kp.max_steps;
+                if (!done && cy < kp.done_y) done = 1;
+                if (!done && steps > 100) done = (sb & gmask) == gmask;
+                o.done[wg] = (uint8_t)done;
+            }
+            if (o.centroid) { o.centroid[3 * wg] = midx; o.centroid[3 * wg + 1] = midy; o.centroid[3 * wg + 2] = midz; }
+            if (o.energy) o.energy[wg] = 0.5f * ksum + psum;
+        }
+        __syncthreads();     // edge phase LDS reads done: pos/vel may be overwritten, t region is free
+        if (is_mass) {
+            s.pos[3 * tid] = px; s.pos[3 * tid + 1] = py; s.pos[3 * tid + 2] = pz;
+            s.vel[3 * tid] = vx; s.vel[3 * tid + 1] = vy; s.vel[3 * tid + 2] = vz;
+        }
+        if (o.obs) {
+            constexpr int d = IN3D ? 3 : 2, per = 3 * d;
+            const int stride = o.obs_stride, nmid = kp.conmid ? 3 : 0;
+            float *tile_obs = reinterpret_cast<float *>(s.t);
+            if (is_mass) {
+                float *row = tile_obs + (size_t)my_wl * stride + per * my_q;
+                const float pm3[3] = {px, py, pz}, vm3[3] = {vx, vy, vz}, am3[3] = {ax, ay, az};
+                const float mm3[3] = {midx, midy, midz};
+                _Pragma("unroll") for (int c = 0; c < d; c++) {
+                    row[c] = kp.midform ? (pm3[c] - mm3[c]) * kp.pk : pm3[c] * kp.pk;
+                    row[d + c] = vm3[c] * kp.vk;
+                    row[2 * d + c] = am3[c] * kp.ak;
+                }
+                if (my_q == 0) {
+                    float *wrow = tile_obs + (size_t)my_wl * stride;
+                    if (nmid) {
+                        wrow[per * M] = kp.midform ? midx : 0.f; wrow[per * M + 1] = kp.midform ? midy : 0.f;
+                        wrow[per * M + 2] = kp.midform ? midz : 0.f;
+                    }
+                    for (int r = per * M + nmid + A; r < stride; r++) wrow[r] = 0.f;
+                }
+            }
+            if (is_mus) tile_obs[(size_t)mu_wl * stride + per * M + nmid + mu_ua] = x * kp.mk;
+        }
+        __syncthreads();
+        stage_out(b.pos + 3 * P0, s.pos, 3 * nP, tid, T);
+        stage_out(b.vel + 3 * P0, s.vel, 3 * nP, tid, T);
+        if (o.obs) stage_out(o.obs + (size_t)w0 * o.obs_stride, reinterpret_cast<const float *>(s.t), W * o.obs_stride, tid, T);
+        // next iteration writes pos/vel/inc before its first barrier: wait for these reads first
+        __syncthreads();
+    }
+#undef WG_PREFETCH
 }
 
 // reset: v += noise (x, y, z if in3d), steps = 0 (PhysicsEnv.reset, gym/optimized_env.py:53-68)
@@ -793,18 +996,20 @@ int validate(const wg_batch *b) {
 
 Geo uniform_geo(const wg_batch *b, int obs_stride) {
     Geo g;
-    g.threads = NTHREADS;
     // walkers per workgroup: fill the 256 mass lanes, keep edges within EPL registers per lane,
     // and make sure the grid has >= 512 workgroups when the batch allows it.
     int W = std::max(1, NTHREADS / b->M);
     if (b->K > 0) W = std::max(1, std::min(W, EPL * NTHREADS / std::max(1, b->K)));
     while (W > 1 && (b->N + W - 1) / W < 512) W = std::max(1, W / 2);
+    if (const char *fw = getenv("WG_DEBUG_WALKERS_PER_BLOCK")) W = std::max(1, atoi(fw));   // experiments only
     g.W = W;
     const bool shfl_shape = b->M <= 64 && (64 % b->M) == 0 && !(WG_ABLATE & 64);
     for (;;) {
         g.Pcap = g.W * b->M; g.Ecap = g.W * b->K; g.Ucap = g.W * b->A;
         g.tbytes = std::max(g.Ecap * 3 * 8, g.W * std::max(0, obs_stride) * 4);
-        g.lite = (shfl_shape && g.W * b->M <= NTHREADS) ? 1 : 0;
+        g.lite = (shfl_shape && g.W * b->M <= MAXT) ? 1 : 0;
+        g.threads = std::min(MAXT, std::max(64, ((g.W * b->M + 63) / 64) * 64));
+        if (b->K > 0 && g.W * b->K > EPL * g.threads) g.threads = MAXT;
         g.lds = carve_bytes(g);
         if (g.lds <= 64 * 1024 || g.W == 1) break;
         g.W = std::max(1, g.W / 2);
@@ -858,6 +1063,52 @@ int dispatch2(const wg_batch *b, const KParams &kp, bool in3d, const float *a, i
                 : launch<STEP, false, false, PWD, false>(b, kp, a, cols, astride, o, plan, blocks, g, st);
 }
 // register (shuffle) reductions: every walker's masses are adjacent lanes of one wave
+bool stream_disabled() {   // diagnostics: WG_NO_STREAM=1 selects the one-tile-per-workgroup kernel
+    static const bool off = [] { const char *e = getenv("WG_NO_STREAM"); return e && *e && *e != '0'; }();
+    return off;
+}
+
+bool stream_ok(const wg_batch *b, const Geo &g) {
+    return !b->ragged && g.lite && (g.W * b->M) % 4 == 0 && (g.W * b->K) % 4 == 0 && b->N % g.W == 0 &&
+           g.W * b->K <= 4 * g.threads && !(WG_ABLATE & 128) && !stream_disabled();
+}
+
+int stream_blocks(const Geo &g) {
+    static thread_local int cus = 0, dev_cached = -1;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    if (dev != dev_cached) {
+        dev_cached = dev;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+    }
+    // resident workgroups per CU: LDS share and a 16-wave budget (VGPR-bound kernel, 4 waves / SIMD)
+    const int by_lds = std::max(1, (160 * 1024) / std::max(g.lds, 1));
+    const int by_waves = std::max(1, 16 / std::max(1, g.threads / 64));
+    return std::min(by_lds, by_waves) * std::max(cus, 1);
+}
+
+int launch_stream(const wg_batch *b, const KParams &kp, bool in3d, const float *a, int cols, int astride,
+                  const wg_outputs &o, const Geo &g, hipStream_t st) {
+    if (g.lds > LDS_LIMIT) return fail(WG_ERANGE, "workgroup needs %d B of LDS (> 160 KiB)", g.lds);
+    const int ntiles = b->N / g.W;
+    const int grid = std::max(1, std::min(ntiles, stream_blocks(g)));
+    const int ne = (g.W * b->K + g.threads - 1) / g.threads;
+#define WG_LAUNCH_STREAM(D3, NE_)                                                                            \
+    hipLaunchKernelGGL((walker_step_stream<D3, NE_>), dim3(grid), dim3(g.threads), g.lds, st, *b, kp, a, cols, \
+                       astride, o, g, ntiles)
+    if (in3d) {
+        if (ne <= 1) WG_LAUNCH_STREAM(true, 1); else if (ne == 2) WG_LAUNCH_STREAM(true, 2);
+        else if (ne == 3) WG_LAUNCH_STREAM(true, 3); else WG_LAUNCH_STREAM(true, 4);
+    } else {
+        if (ne <= 1) WG_LAUNCH_STREAM(false, 1); else if (ne == 2) WG_LAUNCH_STREAM(false, 2);
+        else if (ne == 3) WG_LAUNCH_STREAM(false, 3); else WG_LAUNCH_STREAM(false, 4);
+    }
+#undef WG_LAUNCH_STREAM
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(WG_EHIP, "launch failed: %s", hipGetErrorString(e));
+    return 0;
+}
+
 template <bool STEP>
 int dispatch(const wg_batch *b, const KParams &kp, bool in3d, const float *a, int cols, int astride,
              const wg_outputs &o, const int32_t *plan, int blocks, const Geo &g, hipStream_t st) {
@@ -880,7 +1131,7 @@ int run(const wg_batch *b, const wg_params *p, const float *action, int32_t cols
     if (out.obs && out.obs_stride <= 0) return fail(WG_EINVAL, "obs_stride must be > 0");
     const KParams kp = make_kparams(*p);
     const Geo g = b->ragged ? ragged_geo(b) : uniform_geo(b, out.obs ? out.obs_stride : 0);
-    if (g.W > NTHREADS) return fail(WG_ERANGE, "more than %d walkers per workgroup", NTHREADS);
+    if (g.W > g.threads) return fail(WG_ERANGE, "more than %d walkers per workgroup", g.threads);
     const int blocks = b->ragged ? plan_blocks : (b->N + g.W - 1) / g.W;
     for (int s = 0; s < n_steps; s++) {
         wg_outputs os = out;
@@ -890,6 +1141,11 @@ int run(const wg_batch *b, const wg_params *p, const float *action, int32_t cols
         if (os.energy) os.energy += s * os.out_step;
         if (os.centroid) os.centroid += 3 * s * os.out_step;
         const float *a = action ? action + s * astep : nullptr;
+        if (step && stream_ok(b, g)) {
+            rc = launch_stream(b, kp, p->in3d != 0, a, cols, astride, os, g, stream);
+            if (rc) return rc;
+            continue;
+        }
         rc = step ? dispatch<true>(b, kp, p->in3d != 0, a, cols, astride, os, plan, blocks, g, stream)
                   : dispatch<false>(b, kp, p->in3d != 0, nullptr, 0, 0, os, plan, blocks, g, stream);
         if (rc) return rc;

@@ -84,6 +84,7 @@ struct Geo {
     float invM, invK, invA;    // uniform batches: 1/M, 1/K, 1/A for exact small-int division (fdiv)
     int tbytes;                // spring-term region, also the obs tile of uniform batches (aliased)
     int lite;                  // register-reduction kernels: no LDS for acc, m, reduction terms, offsets
+    int stage;                 // streaming kernel: df region doubles as the pos/vel/acc out-staging tile
 };
 
 struct Carve {
@@ -105,7 +106,8 @@ __host__ __device__ inline int carve_walk(const Geo &g, char *base, Carve *c) {
     auto take = [&](int bytes) { char *p = base ? base + b : nullptr; b += align16(bytes); return p; };
     const int full = g.lite ? 0 : 1;
     char *t = take(g.tbytes), *pos = take(g.Pcap * 12), *vel = take(g.Pcap * 12);
-    char *acc = take(full * g.Pcap * 12), *m = take(full * g.Pcap * 4), *df = take(g.Ecap * 12);
+    char *acc = take(full * g.Pcap * 12), *m = take(full * g.Pcap * 4);
+    char *df = take(std::max(g.Ecap * 12, g.stage * g.Pcap * 36));   // streaming kernel: also the out-stage
     char *inc = take(g.Ecap * 4 + 16), *x = take(g.Ucap * 4);
     char *nrm = take(full * g.Pcap * 4), *ke = take(full * g.Pcap * 4), *pe = take(full * g.Pcap * 4);
     char *red = take(full * g.W * 32);
@@ -186,10 +188,10 @@ __device__ inline int locate(const int *off, int n, int x) {  // largest w with 
 
 // exact idx / d for 0 <= idx < 2^24 via a float reciprocal and one correction
 __device__ inline int fdiv(int idx, int d, float inv) {
-    int q = (int)((float)idx * inv);
-    if (q * d > idx) q--;
-    else if ((q + 1) * d <= idx) q++;
-    return q;
+    // floor(idx / d) for 0 <= idx < 2^22, inv = RN32(1/d): (idx + 1/2)/d sits at least 1/(2d) from an
+    // integer, and the two float roundings move it by less than (idx + 1/2)/d * 2^-23 < 1/(2d).
+    (void)d;
+    return (int)(((float)idx + 0.5f) * inv);
 }
 
 // ---- exact IEEE quotients from one precomputed reciprocal (validated exhaustively-random on the host,
@@ -206,6 +208,19 @@ __device__ inline float fdiv_exact(float x, double y) { return (float)((double)x
 __device__ inline float fdiv_mk(float x, float m, float yf) {
     const float q = x * yf;
     if (!__builtin_isfinite(q) || yf == 0.f) return q;
+    return __builtin_fmaf(__builtin_fmaf(-q, m, x), yf, q);
+}
+__device__ inline float fxsign(float v, uint32_t s) { return __uint_as_float(__float_as_uint(v) ^ s); }
+__device__ inline double dxsign(double v, uint32_t s) {
+    return __hiloint2double(__double2hiint(v) ^ (int)s, __double2loint(v));
+}
+// Unguarded forms (finite operands and quotient): callers detect a non-finite result afterwards.
+__device__ inline double ddiv_fast(double a, double b, double y) {
+    const double q = a * y;
+    return __builtin_fma(__builtin_fma(-q, b, a), y, q);
+}
+__device__ inline float fdiv_fast(float x, float m, float yf) {
+    const float q = x * yf;
     return __builtin_fmaf(__builtin_fmaf(-q, m, x), yf, q);
 }
 __device__ inline double ddiv_exact(double a, double b, double y) {
@@ -263,25 +278,32 @@ __device__ __forceinline__ void spring_edge(const EdgeRec &e, int le, int lm, fl
     double dist = (double)cur;                                      // engine.py:73
     if (CONFIG_R > dist) dist = CONFIG_R;                           // max(distance, r)
     const double yc = 1.0 / dist;
-    float d0 = r0, d1 = r1, d2 = r2;
-    if (cur > 0.f) {                                                // optimized_walker.py:93
-        if ((double)cur == dist) {
-            const float ycf = (float)yc;
-            d0 = fdiv_mk(r0, cur, ycf); d1 = fdiv_mk(r1, cur, ycf); d2 = fdiv_mk(r2, cur, ycf);
-        } else {
-            d0 = r0 / cur; d1 = r1 / cur; d2 = r2 / cur;
-        }
-    }
+    const float fsz = (spring_mode == 1 || !(dx < 0.f && edge_string(e.ij))) ? (-dx) * e.k : 0.f;  // :97-100
+    const float nf = -fsz;                                                                           // :75
+    // Fast path: Markstein quotients from one reciprocal, unguarded; exact whenever the distance is
+    // unclamped and every quotient is finite (otherwise the cold branch redoes this edge with IEEE
+    // divisions).  d = r / cur in float32 (optimized_walker.py:93), t = (nf * r) / dist in float64.
+    const float ycf = (float)yc;
+    float d0 = fdiv_fast(r0, cur, ycf), d1 = fdiv_fast(r1, cur, ycf), d2 = fdiv_fast(r2, cur, ycf);
     double t0, t1, t2;
-    if (spring_mode == 1) {
-        const float fs = (-dx) * e.k;
-        t0 = (double)(fs * d0); t1 = (double)(fs * d1); t2 = (double)(fs * d2);
+    if (spring_mode == 1) {                                          // G2 element: float32, inverted sign
+        t0 = (double)(fsz * d0); t1 = (double)(fsz * d1); t2 = (double)(fsz * d2);
     } else {
-        const float fsz = (dx < 0.f && edge_string(e.ij)) ? 0.f : (-dx) * e.k;   // engine.py:97-100
-        const float nf = -fsz;                                                    // engine.py:75
-        t0 = ddiv_exact((double)(nf * r0), dist, yc);
-        t1 = ddiv_exact((double)(nf * r1), dist, yc);
-        t2 = ddiv_exact((double)(nf * r2), dist, yc);
+        t0 = ddiv_fast((double)(nf * r0), dist, yc);
+        t1 = ddiv_fast((double)(nf * r1), dist, yc);
+        t2 = ddiv_fast((double)(nf * r2), dist, yc);
+    }
+    const bool fast_ok = cur > 0.f && (double)cur == dist && __builtin_isfinite(d0) && __builtin_isfinite(d1) &&
+                         __builtin_isfinite(d2) && __builtin_isfinite(t0) && __builtin_isfinite(t1) &&
+                         __builtin_isfinite(t2);
+    if (__builtin_expect(!fast_ok, 0)) {
+        d0 = r0; d1 = r1; d2 = r2;
+        if (cur > 0.f) { d0 = r0 / cur; d1 = r1 / cur; d2 = r2 / cur; }
+        if (spring_mode == 1) {
+            t0 = (double)(fsz * d0); t1 = (double)(fsz * d1); t2 = (double)(fsz * d2);
+        } else {
+            t0 = (double)(nf * r0) / dist; t1 = (double)(nf * r1) / dist; t2 = (double)(nf * r2) / dist;
+        }
     }
     st[3 * le] = t0; st[3 * le + 1] = t1; st[3 * le + 2] = t2;
     const float dk = np_dot3(vix - vjx, viy - vjy, viz - vjz, d0, d1, d2);  // :102-103
@@ -302,29 +324,63 @@ __device__ __forceinline__ void mass_step(const KParams &kp, const double *st, c
     const double ym = 1.0 / md;      // one IEEE division per mass; every /m below is exact from it
     const float ymf = (float)ym;     // = RN32(1/m)
     ax = 0.f; ay = 0.f; az = 0.f;
-    for (int r = s0; r < s1; r++) {
-        const int ent = inc[r];
-        const int le = lb + (ent >> 1);
-        const bool end_j = ent & 1;
-        const double t0 = st[3 * le], t1 = st[3 * le + 1], t2 = st[3 * le + 2];
-        const float f0 = sdf[3 * le], f1 = sdf[3 * le + 1], f2 = sdf[3 * le + 2];
-        if (kp.spring_mode == 1) {
-            const float sg = end_j ? -1.f : 1.f;
-            ax = ax + fdiv_mk(sg * (float)t0, mf, ymf);
-            ay = ay + fdiv_mk(sg * (float)t1, mf, ymf);
-            az = az + fdiv_mk(sg * (float)t2, mf, ymf);
-        } else {
-            // Point.forced with a float64 force: a = f32(f64(a) + t/m)   (engine.py:67,75)
-            const double sg = end_j ? -1.0 : 1.0;
-            ax = (float)((double)ax + ddiv_exact(sg * t0, md, ym));
-            ay = (float)((double)ay + ddiv_exact(sg * t1, md, ym));
-            az = (float)((double)az + ddiv_exact(sg * t2, md, ym));
+    // Both ends of an edge see the same spring term t and damping force df with opposite signs; the
+    // divisions are odd functions (RN is sign-symmetric), so the quotient is formed once and its sign
+    // flipped by one XOR: -(t/m) == (-t)/m exactly, a + (-d) == a - d.
+    if (kp.spring_mode == 1) {
+        for (int r = s0; r < s1; r++) {
+            const int ent = inc[r];
+            const int le = lb + (ent >> 1);
+            const uint32_t sj = (uint32_t)(ent & 1) << 31;   // sign of the spring term at this end
+            const double *t = st + 3 * le;
+            const float *f = sdf + 3 * le;
+            ax = ax + fxsign(fdiv_mk((float)t[0], mf, ymf), sj);
+            ay = ay + fxsign(fdiv_mk((float)t[1], mf, ymf), sj);
+            az = az + fxsign(fdiv_mk((float)t[2], mf, ymf), sj);
+            const uint32_t sd = sj ^ 0x80000000u;          // damping: p1 gets -df, p2 gets +df
+            ax = ax + fxsign(fdiv_mk(f[0], mf, ymf), sd);
+            ay = ay + fxsign(fdiv_mk(f[1], mf, ymf), sd);
+            az = az + fxsign(fdiv_mk(f[2], mf, ymf), sd);
         }
-        // damping: p1.forced(-damp_force); p2.forced(damp_force)  (optimized_walker.py:105-106)
-        const float sf = end_j ? 1.f : -1.f;
-        ax = ax + fdiv_mk(sf * f0, mf, ymf);
-        ay = ay + fdiv_mk(sf * f1, mf, ymf);
-        az = az + fdiv_mk(sf * f2, mf, ymf);
+    } else {
+        // Fast path: the Markstein quotients without their non-finite guards.  They differ from the
+        // IEEE quotient only when q = t*RN(1/m) is not finite, and then the running sum becomes (and
+        // stays) inf/NaN — so a finite result proves every quotient was exact.  A lane whose result is
+        // not finite redoes its list with plain IEEE divisions (wave-uniform branch, cold).
+        for (int r = s0; r < s1; r++) {
+            const int ent = inc[r];
+            const int le = lb + (ent >> 1);
+            const uint32_t sj = (uint32_t)(ent & 1) << 31;
+            const double *t = st + 3 * le;
+            const float *f = sdf + 3 * le;
+            // Point.forced with a float64 force: a = f32(f64(a) + t/m)   (engine.py:67,75)
+            ax = (float)((double)ax + dxsign(ddiv_fast(t[0], md, ym), sj));
+            ay = (float)((double)ay + dxsign(ddiv_fast(t[1], md, ym), sj));
+            az = (float)((double)az + dxsign(ddiv_fast(t[2], md, ym), sj));
+            // damping: p1.forced(-damp_force); p2.forced(damp_force)  (optimized_walker.py:105-106)
+            const uint32_t sd = sj ^ 0x80000000u;
+            ax = ax + fxsign(fdiv_fast(f[0], mf, ymf), sd);
+            ay = ay + fxsign(fdiv_fast(f[1], mf, ymf), sd);
+            az = az + fxsign(fdiv_fast(f[2], mf, ymf), sd);
+        }
+        const bool bad = !(__builtin_isfinite(ax) && __builtin_isfinite(ay) && __builtin_isfinite(az));
+        if (__builtin_expect(bad, 0)) {
+            ax = 0.f; ay = 0.f; az = 0.f;
+            for (int r = s0; r < s1; r++) {
+                const int ent = inc[r];
+                const int le = lb + (ent >> 1);
+                const uint32_t sj = (uint32_t)(ent & 1) << 31;
+                const double *t = st + 3 * le;
+                const float *f = sdf + 3 * le;
+                ax = (float)((double)ax + dxsign(t[0] / md, sj));
+                ay = (float)((double)ay + dxsign(t[1] / md, sj));
+                az = (float)((double)az + dxsign(t[2] / md, sj));
+                const uint32_t sd = sj ^ 0x80000000u;
+                ax = ax + fxsign(f[0] / mf, sd);
+                ay = ay + fxsign(f[1] / mf, sd);
+                az = az + fxsign(f[2] / mf, sd);
+            }
+        }
     }
     vx = v3[0]; vy = v3[1]; vz = v3[2];
     px = p3[0]; py = p3[1]; pz = p3[2];
@@ -352,17 +408,42 @@ __device__ __forceinline__ void mass_step(const KParams &kp, const double *st, c
 // no extra barrier (north_star: "wavefront shuffles for per-walker reductions").
 __device__ inline float lane_get(float v, int src) { return __shfl(v, src, 64); }
 
-// sequential float sum x_0 + x_1 + ... over the walker's M lanes (base = its first lane)
+// DPP lane moves (one VALU source modifier, no LDS traffic): row_shr:1 0x111, row_ror:8 0x128,
+// wave_shr:1 0x138, quad_perm [1,0,3,2] 0xB1 / [2,3,0,1] 0x4E, row_half_mirror 0x141.
+template <int CTRL> __device__ inline float dpp_f(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+
+// Sequential float sums ((0 + x_0) + x_1) + ... + x_{M-1} over the walker's M lanes, three at once.
+// Chain: s_q <- s_{q-1} + x_q repeated M-1 times leaves lane base+M-1 holding exactly that left-to-right
+// sum of its own walker (the chain never leaves the walker's lanes); then one broadcast per sum.
+__device__ inline void seq_sum3_lanes(float x, float y, float z, int base, int M, float &sx, float &sy, float &sz) {
+    float a = 0.f + x, b = 0.f + y, c = 0.f + z;
+    if (M <= 16) {            // walkers of M | 16 lanes sit inside one 16-lane DPP row
+        for (int t = 1; t < M; t++) { a = dpp_f<0x111>(a) + x; b = dpp_f<0x111>(b) + y; c = dpp_f<0x111>(c) + z; }
+    } else {
+        for (int t = 1; t < M; t++) { a = dpp_f<0x138>(a) + x; b = dpp_f<0x138>(b) + y; c = dpp_f<0x138>(c) + z; }
+    }
+    const int last = base + M - 1;
+    sx = lane_get(a, last); sy = lane_get(b, last); sz = lane_get(c, last);
+}
 __device__ inline float seq_sum_lanes(float x, int base, int M) {
-    float r = 0.f;
-    for (int q = 0; q < M; q++) r += lane_get(x, base + q);
-    return r;
+    float a, b, c;
+    seq_sum3_lanes(x, 0.f, 0.f, base, M, a, b, c);
+    return a;
 }
 // numpy pairwise sum over the walker's M lanes (M divides 64): < 8 sequential; otherwise 8 interleaved
-// partial sums r_j = x_j + x_{j+8} + ... then ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) — the xor-1/2/4
-// butterflies form exactly that tree (IEEE addition is commutative); M % 8 == 0, no remainder loop.
+// partial sums r_j = x_j + x_{j+8} + ... then ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)).  For M = 8, 16 the
+// partials and the tree are DPP moves (row_ror:8, then quad_perm xor-1, xor-2 and row_half_mirror,
+// which pairs each lane of one 4-lane half with a lane of the other: IEEE addition is commutative).
 __device__ inline float pw_sum_lanes(float x, int base, int M, int lane) {
     if (M < 8) return seq_sum_lanes(x, base, M);
+    if (M <= 16) {
+        float r = (M == 16) ? x + dpp_f<0x128>(x) : x;
+        r = r + dpp_f<0xB1>(r);
+        r = r + dpp_f<0x4E>(r);
+        return r + dpp_f<0x141>(r);
+    }
     const int j = (lane - base) & 7;
     float r = lane_get(x, base + j);
     for (int k = 8; k < M; k += 8) r += lane_get(x, base + j + k);
@@ -580,8 +661,8 @@ __global__ __launch_bounds__(MAXT) void walker_step_kernel(
     if (SHFL) {
         const int M = b.M;
         const int gbase = (tid & ~63) + ((lane / M) * M);
-        const float sx = seq_sum_lanes(px, gbase, M), sy = seq_sum_lanes(py, gbase, M),
-                    sz = seq_sum_lanes(pz, gbase, M);
+        float sx, sy, sz;
+        seq_sum3_lanes(px, py, pz, gbase, M, sx, sy, sz);
         const float ysum = pw_sum_lanes(py, gbase, M, lane), vsum = pw_sum_lanes(nv, gbase, M, lane);
         const float ksum = pw_sum_lanes(ke, gbase, M, lane), psum = pw_sum_lanes(pe, gbase, M, lane);
         const unsigned long long gmask = (M == 64) ? ~0ull : (((1ull << M) - 1ull) << (gbase & 63));
@@ -765,29 +846,38 @@ typedef unsigned vu4 __attribute__((ext_vector_type(4)));
 typedef float vf2 __attribute__((ext_vector_type(2)));
 
 template <bool IN3D, int NE>
-__global__ __launch_bounds__(MAXT) void walker_step_stream(
+__global__ __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(4, 8))) void walker_step_stream(
     wg_batch b, KParams kp, const float *__restrict__ action, int action_cols, int action_stride,
     wg_outputs o, Geo geo, int ntiles) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const Carve s = carve(smem, geo);
-    const int tid = threadIdx.x, lane = tid & 63, T = blockDim.x;
+    const int T = blockDim.x;
     const int W = geo.W, M = b.M, K = b.K, A = b.A;
     const int nP = W * M, nE = W * K, nU = W * A;
-    // fixed lane roles
-    const bool is_mass = tid < nP, is_mus = tid < nU;
-    const int my_wl = fdiv(tid, M, geo.invM), my_q = tid - my_wl * M;
-    const int gbase = (tid & ~63) + ((lane / M) * M);            // first lane of my walker in this wave
-    const int mu_wl = A > 0 ? fdiv(tid, A, geo.invA) : 0, mu_ua = tid - mu_wl * A;
-    const bool acts = action != nullptr && is_mus && mu_ua < action_cols;
-    const int n3 = 3 * nP / 4, n1 = nP / 4, ni = nE / 4;
-    // clamped per-lane indices: every prefetch load is unconditional (no branches around loads)
-    const int i3 = min(tid, n3 - 1), i1 = min(tid, n1 - 1), ii = min(tid, max(ni - 1, 0));
-    const int iu = min(tid, max(nU - 1, 0)), iw = min(my_wl, W - 1), iq = min(my_q, M - 1);
-    const int iau = min(mu_ua, max(A - 1, 0)), iaw = min(mu_wl, W - 1);
+    const int n3 = 3 * nP / 4, ni = nE / 4;
+    // Fixed lane roles.  Re-derived inside the tile loop from an opaque copy of the lane id: if they
+    // were loop invariants the compiler would keep ~80 of them live in VGPRs across the whole loop.
+#define WG_LANE_ROLES(tid_expr)                                                                            \
+    const int tid = (tid_expr), lane = tid & 63;                                                            \
+    const bool is_mass = tid < nP, is_mus = tid < nU;                                                       \
+    const int my_wl = fdiv(tid, M, geo.invM), my_q = tid - my_wl * M;                                       \
+    const int gbase = (tid & ~63) + ((lane / M) * M);            /* first lane of my walker in the wave */  \
+    const int mu_wl = A > 0 ? fdiv(tid, A, geo.invA) : 0, mu_ua = tid - mu_wl * A;                          \
+    const bool acts = action != nullptr && is_mus && mu_ua < action_cols;                                   \
+    /* clamped per-lane indices: every prefetch load is unconditional (no branches around loads) */         \
+    const int i3 = min(tid, n3 - 1), ii = min(tid, max(ni - 1, 0));                                         \
+    const int iu = min(tid, max(nU - 1, 0)), iw = min(my_wl, W - 1), iq = min(my_q, M - 1);                 \
+    const int iau = min(mu_ua, max(A - 1, 0)), iaw = min(mu_wl, W - 1);                                     \
+    (void)is_mass; (void)is_mus; (void)acts; (void)gbase; (void)i3; (void)ii; (void)iu; (void)iw; (void)iq;  \
+    (void)iau; (void)iaw
 
+    // prefetch registers: tile t + gridDim.x, loaded while tile t computes
     vf4 pp, pv; vu4 pi = vu4{0u, 0u, 0u, 0u}; vu4 pe[NE];
     float pm, pmx = 0.f, pact = 0.f, pst = 0.f; vf2 pbd = vf2{0.f, 0.f};
     uint32_t pio = 0u; int psteps;
+    // current-tile registers (the records the compute reads outside LDS)
+    vu4 ce[NE];
+    float mf, bx, ba, bst; vf2 bd; uint32_t io; int wsteps;
 #define WG_PREFETCH(tile_)                                                                                  \
     do {                                                                                                    \
         const int w0_ = (tile_) * W;                                                                        \
@@ -812,23 +902,33 @@ __global__ __launch_bounds__(MAXT) void walker_step_stream(
         }                                                                                                    \
         psteps = b.steps[w0_ + iw];                                                                          \
     } while (0)
+    // commit: prefetched state -> LDS (pos, vel, incidence), records -> current-tile registers
+#define WG_COMMIT()                                                                                         \
+    do {                                                                                                    \
+        if (tid < n3) { reinterpret_cast<vf4 *>(s.pos)[tid] = pp; reinterpret_cast<vf4 *>(s.vel)[tid] = pv; } \
+        if (tid < ni) reinterpret_cast<vu4 *>(s.inc)[tid] = pi;                                              \
+        _Pragma("unroll") for (int it = 0; it < NE; it++) ce[it] = pe[it];                                   \
+        mf = pm; bx = pmx; ba = pact; bst = pst; bd = pbd; io = pio; wsteps = psteps;                       \
+    } while (0)
 
     int tile = blockIdx.x;
-    if (tile < ntiles) WG_PREFETCH(tile);
+    if (tile >= ntiles) return;
+    {
+        WG_LANE_ROLES((int)threadIdx.x);
+        WG_PREFETCH(tile);
+        WG_COMMIT();
+        if (tile + (int)gridDim.x < ntiles) WG_PREFETCH(tile + (int)gridDim.x);
+    }
+    // Per tile: compute from LDS + current registers; then commit the (long since landed) prefetch and
+    // issue the next one BEFORE this tile's stores, so no load is ever waited on behind a store.
     for (; tile < ntiles; tile += gridDim.x) {
+        int tid_opaque = threadIdx.x;
+        asm volatile("" : "+v"(tid_opaque));
+        WG_LANE_ROLES(tid_opaque);
         const int w0 = tile * W;
         const size_t P0 = (size_t)w0 * M, U0 = (size_t)w0 * A;
-        // ---- commit the prefetched tile: state to LDS, records to this iteration's registers
-        if (tid < n3) { reinterpret_cast<vf4 *>(s.pos)[tid] = pp; reinterpret_cast<vf4 *>(s.vel)[tid] = pv; }
-        if (tid < ni) reinterpret_cast<vu4 *>(s.inc)[tid] = pi;
-        vu4 ce[NE];
-        _Pragma("unroll") for (int it = 0; it < NE; it++) ce[it] = pe[it];
-        const float mf = pm, bx = pmx, ba = pact, bst = pst;
-        const vf2 bd = pbd;
-        const uint32_t io = pio;
-        const int wsteps = psteps;
-        // ---- the next tile's loads go in flight now
-        if (tile + (int)gridDim.x < ntiles) WG_PREFETCH(tile + (int)gridDim.x);
+        const bool has_next = tile + (int)gridDim.x < ntiles;
+        const int steps = wsteps + 1;   // this tile's (wsteps is overwritten by the commit below)
 
         // ---- act (gym/optimized_walker.py:27-43,164-172)
         float x = bx;
@@ -836,10 +936,9 @@ __global__ __launch_bounds__(MAXT) void walker_step_stream(
             x = (kp.action_mode == 1) ? ((ba != 0.f) ? x + bst : x - bst) : x + ba;
             if (bd.x > x) x = bd.x;     // Python max(x, originx*minl)
             if (bd.y < x) x = bd.y;     // Python min(x, originx*maxl)
-            b.muscle_x[U0 + tid] = x;
         }
         if (is_mus) s.x[tid] = x;
-        __syncthreads();
+        __syncthreads();   // also: the previous tile's stage-out reads of t/df/spos are done
 
         // ---- edge phase
         _Pragma("unroll") for (int it = 0; it < NE; it++) {
@@ -855,20 +954,18 @@ __global__ __launch_bounds__(MAXT) void walker_step_stream(
         // ---- mass phase
         float px = 0.f, py = 0.f, pz = 0.f, vx = 0.f, vy = 0.f, vz = 0.f, ax = 0.f, ay = 0.f, az = 0.f;
         float nv = 0.f, ke = 0.f, pe_ = 0.f;
+        bool hit = false;
         if (is_mass) {
-            bool hit;
             const int lb = my_wl * K;
             mass_step(kp, s.t, s.df, reinterpret_cast<const uint16_t *>(s.inc) + 2 * lb, lb, (int)(io & 0xffffu),
                       (int)(io >> 16), mf, s.pos + 3 * tid, s.vel + 3 * tid, px, py, pz, vx, vy, vz, ax, ay, az, hit);
-            if (b.contact) b.contact[P0 + tid] = (uint8_t)hit;
-            float *ga = b.acc + 3 * (P0 + tid);
-            ga[0] = ax; ga[1] = ay; ga[2] = az;
             nv = np_norm3(vx, vy, vz);
             ke = mf * (nv * nv);     // numpy's float32 ** 2 is libm powf: may differ by 1 ulp
             pe_ = (float)((double)mf * kp.g) * (py - kp.ground);
         }
         // per-walker reductions in registers (all lanes of the wave take part in the shuffles)
-        const float sx = seq_sum_lanes(px, gbase, M), sy = seq_sum_lanes(py, gbase, M), sz = seq_sum_lanes(pz, gbase, M);
+        float sx, sy, sz;
+        seq_sum3_lanes(px, py, pz, gbase, M, sx, sy, sz);
         const float ysum = pw_sum_lanes(py, gbase, M, lane), vsum = pw_sum_lanes(nv, gbase, M, lane);
         const float ksum = pw_sum_lanes(ke, gbase, M, lane), psum = pw_sum_lanes(pe_, gbase, M, lane);
         const unsigned long long gmask = (M == 64) ? ~0ull : (((1ull << M) - 1ull) << (gbase & 63));
@@ -876,28 +973,12 @@ __global__ __launch_bounds__(MAXT) void walker_step_stream(
         const unsigned long long sb = __ballot(is_mass && nv < 0.1f);
         const float fM = (float)M;
         const float midx = sx / fM, midy = sy / fM, midz = sz / fM;
-        if (is_mass && my_q == 0) {                                   // gym/optimized_env.py:189-248
-            const size_t wg = (size_t)(w0 + my_wl);
-            const int steps = wsteps + 1;
-            b.steps[wg] = steps;
-            const float cy = ysum / fM;
-            if (o.reward) {
-                const float vpen = (-(vsum / fM)) * 0.1f;
-                o.reward[wg] = (cy + vpen) + (float)(-(double)__popcll(hb & gmask) * 0.5);
-            }
-            if (o.done) {
-                int done = steps >= kp.max_steps;
-                if (!done && cy < kp.done_y) done = 1;
-                if (!done && steps > 100) done = (sb & gmask) == gmask;
-                o.done[wg] = (uint8_t)done;
-            }
-            if (o.centroid) { o.centroid[3 * wg] = midx; o.centroid[3 * wg + 1] = midy; o.centroid[3 * wg + 2] = midz; }
-            if (o.energy) o.energy[wg] = 0.5f * ksum + psum;
-        }
-        __syncthreads();     // edge phase LDS reads done: pos/vel may be overwritten, t region is free
-        if (is_mass) {
-            s.pos[3 * tid] = px; s.pos[3 * tid + 1] = py; s.pos[3 * tid + 2] = pz;
-            s.vel[3 * tid] = vx; s.vel[3 * tid + 1] = vy; s.vel[3 * tid + 2] = vz;
+        __syncthreads();     // edge/mass LDS reads done: t, pos, vel, inc are free
+        if (is_mass) {    // out-stage tile in the (now free) damping-force region: pos | vel | acc
+            float *sp = s.df + 3 * tid, *sv = s.df + 3 * nP + 3 * tid, *sa = s.df + 6 * nP + 3 * tid;
+            sp[0] = px; sp[1] = py; sp[2] = pz;
+            sv[0] = vx; sv[1] = vy; sv[2] = vz;
+            sa[0] = ax; sa[1] = ay; sa[2] = az;
         }
         if (o.obs) {
             constexpr int d = IN3D ? 3 : 2, per = 3 * d;
@@ -923,14 +1004,42 @@ __global__ __launch_bounds__(MAXT) void walker_step_stream(
             }
             if (is_mus) tile_obs[(size_t)mu_wl * stride + per * M + nmid + mu_ua] = x * kp.mk;
         }
+        // ---- next tile: commit the prefetch (landed during this tile's compute), issue the one after
+        if (has_next) {
+            WG_COMMIT();
+            if (tile + 2 * (int)gridDim.x < ntiles) WG_PREFETCH(tile + 2 * (int)gridDim.x);
+        }
         __syncthreads();
-        stage_out(b.pos + 3 * P0, s.pos, 3 * nP, tid, T);
-        stage_out(b.vel + 3 * P0, s.vel, 3 * nP, tid, T);
+        // ---- this tile's stores
+        if (acts) b.muscle_x[U0 + tid] = x;
+        if (is_mass) {
+            if (b.contact) b.contact[P0 + tid] = (uint8_t)hit;
+            if (my_q == 0) {                                          // gym/optimized_env.py:189-248
+                const size_t wg = (size_t)(w0 + my_wl);
+                b.steps[wg] = steps;
+                const float cy = ysum / fM;
+                if (o.reward) {
+                    const float vpen = (-(vsum / fM)) * 0.1f;
+                    o.reward[wg] = (cy + vpen) + (float)(-(double)__popcll(hb & gmask) * 0.5);
+                }
+                if (o.done) {
+                    int done = steps >= kp.max_steps;
+                    if (!done && cy < kp.done_y) done = 1;
+                    if (!done && steps > 100) done = (sb & gmask) == gmask;
+                    o.done[wg] = (uint8_t)done;
+                }
+                if (o.centroid) { o.centroid[3 * wg] = midx; o.centroid[3 * wg + 1] = midy; o.centroid[3 * wg + 2] = midz; }
+                if (o.energy) o.energy[wg] = 0.5f * ksum + psum;
+            }
+        }
+        stage_out(b.pos + 3 * P0, s.df, 3 * nP, tid, T);
+        stage_out(b.vel + 3 * P0, s.df + 3 * nP, 3 * nP, tid, T);
+        stage_out(b.acc + 3 * P0, s.df + 6 * nP, 3 * nP, tid, T);
         if (o.obs) stage_out(o.obs + (size_t)w0 * o.obs_stride, reinterpret_cast<const float *>(s.t), W * o.obs_stride, tid, T);
-        // next iteration writes pos/vel/inc before its first barrier: wait for these reads first
-        __syncthreads();
     }
 #undef WG_PREFETCH
+#undef WG_COMMIT
+#undef WG_LANE_ROLES
 }
 
 // reset: v += noise (x, y, z if in3d), steps = 0 (PhysicsEnv.reset, gym/optimized_env.py:53-68)
@@ -995,7 +1104,7 @@ int validate(const wg_batch *b) {
 }
 
 Geo uniform_geo(const wg_batch *b, int obs_stride) {
-    Geo g;
+    Geo g{};
     // walkers per workgroup: fill the 256 mass lanes, keep edges within EPL registers per lane,
     // and make sure the grid has >= 512 workgroups when the batch allows it.
     int W = std::max(1, NTHREADS / b->M);
@@ -1021,7 +1130,7 @@ Geo uniform_geo(const wg_batch *b, int obs_stride) {
 }
 
 Geo ragged_geo(const wg_batch *b) {
-    Geo g;
+    Geo g{};
     g.threads = NTHREADS;
     g.W = RAG_W;
     g.Pcap = std::max(RAG_P, b->M);
@@ -1063,8 +1172,8 @@ int dispatch2(const wg_batch *b, const KParams &kp, bool in3d, const float *a, i
                 : launch<STEP, false, false, PWD, false>(b, kp, a, cols, astride, o, plan, blocks, g, st);
 }
 // register (shuffle) reductions: every walker's masses are adjacent lanes of one wave
-bool stream_disabled() {   // diagnostics: WG_NO_STREAM=1 selects the one-tile-per-workgroup kernel
-    static const bool off = [] { const char *e = getenv("WG_NO_STREAM"); return e && *e && *e != '0'; }();
+bool stream_disabled() {   // the persistent kernel is opt-in (WG_STREAM=1) until it beats one-tile-per-workgroup
+    static const bool off = [] { const char *e = getenv("WG_STREAM"); return !(e && *e && *e != '0'); }();
     return off;
 }
 
@@ -1089,13 +1198,16 @@ int stream_blocks(const Geo &g) {
 
 int launch_stream(const wg_batch *b, const KParams &kp, bool in3d, const float *a, int cols, int astride,
                   const wg_outputs &o, const Geo &g, hipStream_t st) {
-    if (g.lds > LDS_LIMIT) return fail(WG_ERANGE, "workgroup needs %d B of LDS (> 160 KiB)", g.lds);
+    Geo gs = g;
+    gs.stage = 1;
+    gs.lds = carve_bytes(gs);
+    if (gs.lds > LDS_LIMIT) return fail(WG_ERANGE, "workgroup needs %d B of LDS (> 160 KiB)", gs.lds);
     const int ntiles = b->N / g.W;
-    const int grid = std::max(1, std::min(ntiles, stream_blocks(g)));
+    const int grid = std::max(1, std::min(ntiles, stream_blocks(gs)));
     const int ne = (g.W * b->K + g.threads - 1) / g.threads;
 #define WG_LAUNCH_STREAM(D3, NE_)                                                                            \
-    hipLaunchKernelGGL((walker_step_stream<D3, NE_>), dim3(grid), dim3(g.threads), g.lds, st, *b, kp, a, cols, \
-                       astride, o, g, ntiles)
+    hipLaunchKernelGGL((walker_step_stream<D3, NE_>), dim3(grid), dim3(gs.threads), gs.lds, st, *b, kp, a, cols, \
+                       astride, o, gs, ntiles)
     if (in3d) {
         if (ne <= 1) WG_LAUNCH_STREAM(true, 1); else if (ne == 2) WG_LAUNCH_STREAM(true, 2);
         else if (ne == 3) WG_LAUNCH_STREAM(true, 3); else WG_LAUNCH_STREAM(true, 4);

@@ -9,10 +9,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "build_ablate")
-MASKS = [0, 32]
-EXTRA = {"nt64": ["-DWG_ABLATE=32", "-DWG_NTHREADS=64"], "nt128": ["-DWG_ABLATE=32", "-DWG_NTHREADS=128"],
-         "nt64_noobs": ["-DWG_ABLATE=48", "-DWG_NTHREADS=64"], "nt64_noinc": ["-DWG_ABLATE=34", "-DWG_NTHREADS=64"],
-         "nt64_skel": ["-DWG_ABLATE=59", "-DWG_NTHREADS=64"]}   # name -> extra -D flags
+MASKS = [0, 1, 2, 3, 16, 19]
+EXTRA = {}   # name -> extra -D flags
 
 
 def build():
@@ -28,7 +26,7 @@ def build():
         assert j.wait() == 0
 
 
-def time_one(lib, steps=200, warm=20, n=65536, workload="canonical"):
+def time_one(lib, steps=200, warm=20, n=int(os.environ.get("WG_N", "65536")), workload="canonical"):
     os.environ["WALKER_HIP_LIB"] = lib
     import torch
     from walker_gym_amd.batched_env import BatchedPhysicsEnv
@@ -46,7 +44,7 @@ def run():
     libs = sorted(f for f in os.listdir(OUT) if f.endswith(".so"))
     for f in libs:
         r = subprocess.run([sys.executable, __file__, "one", os.path.join(OUT, f)], capture_output=True, text=True,
-                           timeout=300)
+                           timeout=300, env=dict(os.environ, WG_STREAM="0"))
         print(f"{f:24s} {r.stdout.strip()} {r.stderr.strip()[-200:] if r.returncode else ''}", flush=True)
 
 

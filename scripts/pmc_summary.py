@@ -10,7 +10,7 @@ tag = sys.argv[1] if len(sys.argv) > 1 else "pmc"
 agg = collections.defaultdict(list)
 for f in sorted(glob.glob(f"gpurun_out/{tag}[0-9]*/pmc_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
-        if "walker_step_kernel" in r["Kernel_Name"]:
+        if "walker_step" in r["Kernel_Name"]:
             agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
 out = {k: sum(v) / len(v) for k, v in agg.items()}
 for k, v in sorted(out.items()):

@@ -22,7 +22,7 @@ def build(extra=()):
     subprocess.run(cmd, check=True)
 
 
-def run(n=65536):
+def run(n=int(os.environ.get("WG_N", "65536"))):
     os.environ["WALKER_HIP_LIB"] = LIB
     import torch
     from walker_gym_amd import _lib

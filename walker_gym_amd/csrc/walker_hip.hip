@@ -74,6 +74,7 @@ struct KParams {
     float pk, vk, ak, mk, done_y;
     double g;
     int max_steps, midform, conmid, spring_mode, action_mode;
+    int stagger;    // diagnostics (WG_STAGGER): blocks with blockIdx % 4 == k idle k*stagger*64 cycles first
 };
 
 // Per-launch geometry: caps of one workgroup's slice (LDS carve sizes).
@@ -311,6 +312,26 @@ __device__ __forceinline__ void spring_edge(const EdgeRec &e, int le, int lm, fl
     sdf[3 * le] = dkc * d0; sdf[3 * le + 1] = dkc * d1; sdf[3 * le + 2] = dkc * d2;
 }
 
+// One incidence entry's spring term (float64) and damping force (float32), read from LDS.
+struct IncTerm { double t0, t1, t2; float f0, f1, f2; };
+__device__ __forceinline__ IncTerm inc_term(const double *st, const float *sdf, int lb, int ent) {
+    const int le = lb + (ent >> 1);
+    return IncTerm{st[3 * le], st[3 * le + 1], st[3 * le + 2], sdf[3 * le], sdf[3 * le + 1], sdf[3 * le + 2]};
+}
+// a = f32(f64(a) + t/m) (Point.forced with a float64 force, engine.py:67,75), then the damping pair
+// p1.forced(-df), p2.forced(df) (optimized_walker.py:105-106); end j sees the opposite signs.
+__device__ __forceinline__ void acc_f64_entry(const IncTerm &q, int ent, double md, double ym, float mf, float ymf,
+                                              float &ax, float &ay, float &az) {
+    const uint32_t sj = (uint32_t)(ent & 1) << 31;
+    ax = (float)((double)ax + dxsign(ddiv_fast(q.t0, md, ym), sj));
+    ay = (float)((double)ay + dxsign(ddiv_fast(q.t1, md, ym), sj));
+    az = (float)((double)az + dxsign(ddiv_fast(q.t2, md, ym), sj));
+    const uint32_t sd = sj ^ 0x80000000u;
+    ax = ax + fxsign(fdiv_fast(q.f0, mf, ymf), sd);
+    ay = ay + fxsign(fdiv_fast(q.f1, mf, ymf), sd);
+    az = az + fxsign(fdiv_fast(q.f2, mf, ymf), sd);
+}
+
 // Mass `lp`: the ordered force accumulation over its incidence list (edge order, spring then damping
 // per edge — gym/optimized_walker.py:124-127 with gym/engine.py:65-76, 101-102), then gravity, linear
 // damping and the ground penalty (gym/env.py:31-41 / gym/optimized_env.py:146-172, each one
@@ -347,21 +368,27 @@ __device__ __forceinline__ void mass_step(const KParams &kp, const double *st, c
         // IEEE quotient only when q = t*RN(1/m) is not finite, and then the running sum becomes (and
         // stays) inf/NaN — so a finite result proves every quotient was exact.  A lane whose result is
         // not finite redoes its list with plain IEEE divisions (wave-uniform branch, cold).
-        for (int r = s0; r < s1; r++) {
-            const int ent = inc[r];
-            const int le = lb + (ent >> 1);
-            const uint32_t sj = (uint32_t)(ent & 1) << 31;
-            const double *t = st + 3 * le;
-            const float *f = sdf + 3 * le;
-            // Point.forced with a float64 force: a = f32(f64(a) + t/m)   (engine.py:67,75)
-            ax = (float)((double)ax + dxsign(ddiv_fast(t[0], md, ym), sj));
-            ay = (float)((double)ay + dxsign(ddiv_fast(t[1], md, ym), sj));
-            az = (float)((double)az + dxsign(ddiv_fast(t[2], md, ym), sj));
-            // damping: p1.forced(-damp_force); p2.forced(damp_force)  (optimized_walker.py:105-106)
-            const uint32_t sd = sj ^ 0x80000000u;
-            ax = ax + fxsign(fdiv_fast(f[0], mf, ymf), sd);
-            ay = ay + fxsign(fdiv_fast(f[1], mf, ymf), sd);
-            az = az + fxsign(fdiv_fast(f[2], mf, ymf), sd);
+        // Software-pipelined, two register sets (A, B) in ping-pong: the reads of the next entry are
+        // issued before the arithmetic of the current one, so LDS latency overlaps it.  Reads past the
+        // list end are clamped to its last entry (always a valid address) and their values unused.
+        if (s1 > s0) {
+            const int rl = s1 - 1;
+            int ea = inc[s0], eb = inc[min(s0 + 1, rl)];
+            IncTerm A = inc_term(st, sdf, lb, ea), B;
+            for (int r = s0; r < s1; r += 2) {
+                B = inc_term(st, sdf, lb, eb);
+                const int ea2 = inc[min(r + 2, rl)];
+                __builtin_amdgcn_sched_barrier(0);   // keep the reads above the arithmetic
+                acc_f64_entry(A, ea, md, ym, mf, ymf, ax, ay, az);
+                if (r + 1 >= s1) break;
+                A = inc_term(st, sdf, lb, ea2);
+                const int eb2 = inc[min(r + 3, rl)];
+                __builtin_amdgcn_sched_barrier(0);
+                acc_f64_entry(B, eb, md, ym, mf, ymf, ax, ay, az);
+                ea = ea2; eb = eb2;
+                // opaque hand-over: stops the phi-of-loads fold that would sink A's reads to its use
+                asm volatile("" : "+v"(A.t0), "+v"(A.t1), "+v"(A.t2), "+v"(A.f0), "+v"(A.f1), "+v"(A.f2), "+v"(ea), "+v"(eb));
+            }
         }
         const bool bad = !(__builtin_isfinite(ax) && __builtin_isfinite(ay) && __builtin_isfinite(az));
         if (__builtin_expect(bad, 0)) {
@@ -463,6 +490,10 @@ __global__ __launch_bounds__(MAXT) void walker_step_kernel(
     extern __shared__ __attribute__((aligned(16))) char smem[];
     Carve s = carve(smem, geo);
     const int tid = threadIdx.x, lane = tid & 63, T = blockDim.x;
+    if (kp.stagger > 0) {
+        const int k = (int)(blockIdx.x & 3) * kp.stagger;
+        for (int i = 0; i < k; i++) __builtin_amdgcn_s_sleep(1);
+    }
     STAMP(0);
 
     // ---- this workgroup's walker range and flat slices
@@ -845,7 +876,9 @@ typedef float vf4 __attribute__((ext_vector_type(4)));   // native vectors keep 
 typedef unsigned vu4 __attribute__((ext_vector_type(4)));
 typedef float vf2 __attribute__((ext_vector_type(2)));
 
-template <bool IN3D, int NE>
+// PERSIST = false: one tile per workgroup (grid = tiles), all of the tile's loads issued before any
+// of them is waited on; PERSIST = true: persistent grid with the next tile prefetched (see above).
+template <bool IN3D, int NE, bool PERSIST>
 __global__ __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(4, 8))) void walker_step_stream(
     wg_batch b, KParams kp, const float *__restrict__ action, int action_cols, int action_stride,
     wg_outputs o, Geo geo, int ntiles) {
@@ -917,17 +950,17 @@ __global__ __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(4, 8))) vo
         WG_LANE_ROLES((int)threadIdx.x);
         WG_PREFETCH(tile);
         WG_COMMIT();
-        if (tile + (int)gridDim.x < ntiles) WG_PREFETCH(tile + (int)gridDim.x);
+        if (PERSIST && tile + (int)gridDim.x < ntiles) WG_PREFETCH(tile + (int)gridDim.x);
     }
     // Per tile: compute from LDS + current registers; then commit the (long since landed) prefetch and
     // issue the next one BEFORE this tile's stores, so no load is ever waited on behind a store.
-    for (; tile < ntiles; tile += gridDim.x) {
+    for (; tile < ntiles; tile += PERSIST ? (int)gridDim.x : ntiles) {
         int tid_opaque = threadIdx.x;
         asm volatile("" : "+v"(tid_opaque));
         WG_LANE_ROLES(tid_opaque);
         const int w0 = tile * W;
         const size_t P0 = (size_t)w0 * M, U0 = (size_t)w0 * A;
-        const bool has_next = tile + (int)gridDim.x < ntiles;
+        const bool has_next = PERSIST && tile + (int)gridDim.x < ntiles;
         const int steps = wsteps + 1;   // this tile's (wsteps is overwritten by the commit below)
 
         // ---- act (gym/optimized_walker.py:27-43,164-172)
@@ -1081,6 +1114,8 @@ KParams make_kparams(const wg_params &p) {
     k.g = p.g;
     k.max_steps = p.max_steps; k.midform = p.midform; k.conmid = p.conmid;
     k.spring_mode = p.spring_mode; k.action_mode = p.action_mode;
+    static const int stagger = [] { const char *e = getenv("WG_STAGGER"); return e ? atoi(e) : 0; }();
+    k.stagger = stagger;
     return k;
 }
 
@@ -1172,10 +1207,15 @@ int dispatch2(const wg_batch *b, const KParams &kp, bool in3d, const float *a, i
                 : launch<STEP, false, false, PWD, false>(b, kp, a, cols, astride, o, plan, blocks, g, st);
 }
 // register (shuffle) reductions: every walker's masses are adjacent lanes of one wave
-bool stream_disabled() {   // the persistent kernel is opt-in (WG_STREAM=1) until it beats one-tile-per-workgroup
-    static const bool off = [] { const char *e = getenv("WG_STREAM"); return !(e && *e && *e != '0'); }();
-    return off;
+// Kernel selection for uniform register-reduction batches (diagnostics / A-B runs):
+//   default / WG_STREAM=0 -> walker_step_kernel (staged loads); WG_STREAM=1 -> walker_step_stream one tile per
+//   workgroup; WG_STREAM=2 -> walker_step_stream persistent with next-tile prefetch.
+int stream_mode() {
+    static const int m = [] { const char *e = getenv("WG_STREAM"); return e && *e ? atoi(e) : 0; }();
+    return m;
 }
+bool stream_disabled() { return stream_mode() == 0; }
+bool stream_persist() { return stream_mode() == 2; }
 
 bool stream_ok(const wg_batch *b, const Geo &g) {
     return !b->ragged && g.lite && (g.W * b->M) % 4 == 0 && (g.W * b->K) % 4 == 0 && b->N % g.W == 0 &&
@@ -1203,11 +1243,18 @@ int launch_stream(const wg_batch *b, const KParams &kp, bool in3d, const float *
     gs.lds = carve_bytes(gs);
     if (gs.lds > LDS_LIMIT) return fail(WG_ERANGE, "workgroup needs %d B of LDS (> 160 KiB)", gs.lds);
     const int ntiles = b->N / g.W;
-    const int grid = std::max(1, std::min(ntiles, stream_blocks(gs)));
+    const bool persist = stream_persist();
+    const int grid = persist ? std::max(1, std::min(ntiles, stream_blocks(gs))) : ntiles;
     const int ne = (g.W * b->K + g.threads - 1) / g.threads;
 #define WG_LAUNCH_STREAM(D3, NE_)                                                                            \
-    hipLaunchKernelGGL((walker_step_stream<D3, NE_>), dim3(grid), dim3(gs.threads), gs.lds, st, *b, kp, a, cols, \
-                       astride, o, gs, ntiles)
+    do {                                                                                                     \
+        if (persist)                                                                                         \
+            hipLaunchKernelGGL((walker_step_stream<D3, NE_, true>), dim3(grid), dim3(gs.threads), gs.lds, st, \
+                               *b, kp, a, cols, astride, o, gs, ntiles);                                     \
+        else                                                                                                 \
+            hipLaunchKernelGGL((walker_step_stream<D3, NE_, false>), dim3(grid), dim3(gs.threads), gs.lds, st, \
+                               *b, kp, a, cols, astride, o, gs, ntiles);                                     \
+    } while (0)
     if (in3d) {
         if (ne <= 1) WG_LAUNCH_STREAM(true, 1); else if (ne == 2) WG_LAUNCH_STREAM(true, 2);
         else if (ne == 3) WG_LAUNCH_STREAM(true, 3); else WG_LAUNCH_STREAM(true, 4);

@@ -13,7 +13,7 @@ step() {  # step <name> <timeout_s> <cmd...>
   if [ $rc -ge 2 ] && [ $rc -ne 5 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
-step pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider -x
+step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py --steps 300 --warmup 30
 step rocprof_trace 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 200 --warmup 20 --no-cpu-baseline

@@ -37,7 +37,7 @@ def run(n=int(os.environ.get("WG_N", "65536"))):
     env.run(acts[5:].contiguous(), 1)
     torch.cuda.synchronize()
     nb = env.launch_geometry()["blocks"]
-    st = np.zeros((nb, 8), np.uint64)
+    st = np.zeros((nb, 16), np.uint64)
     assert L.wg_debug_stamps(st.ctypes.data_as(C.c_void_p), nb) == 0
     t = (st[:, :7].astype(np.int64) - int(st[:, 0].min())) / 100.0   # us (100 MHz)
     print(f"blocks {nb}; kernel span {t[:, 6].max():.1f} us; block start spread {t[:, 0].max():.1f} us")
@@ -45,6 +45,11 @@ def run(n=int(os.environ.get("WG_N", "65536"))):
     for k in range(6):
         print(f"  {NAMES[k]:>10s} -> {NAMES[k+1]:<10s} mean {d[:, k].mean():6.2f}  p50 {np.median(d[:, k]):6.2f}"
               f"  p90 {np.percentile(d[:, k], 90):6.2f} us")
+    tt = (st.astype(np.int64) - int(st[:, 0].min())) / 100.0
+    for a, b_, nm in ((2, 10, "edge-end -> mass start (1/m)"), (10, 7, "incidence loop"), (7, 8, "env+run1"),
+                      (8, 9, "stores+norm+seq/pw sums"), (9, 3, "ballots+outputs+barrier")):
+        dd = tt[:, b_] - tt[:, a]
+        print(f"  {nm:>32s} mean {dd.mean():6.2f} p50 {np.median(dd):6.2f} us")
     life = t[:, 6] - t[:, 0]
     print(f"  block lifetime mean {life.mean():.2f} p50 {np.median(life):.2f} p90 {np.percentile(life, 90):.2f}")
     # concurrency profile

@@ -224,3 +224,24 @@ def test_rollout_equals_stepwise():
         torch.cuda.synchronize()
         assert np.array_equal(ob.cpu().numpy(), o[t].cpu().numpy())
         assert np.array_equal(rw.cpu().numpy(), r[t].cpu().numpy())
+
+
+def test_kernel_variants_agree(tmp_path):
+    """The wave-independent lean kernel (default for uniform M | 64 batches) and the workgroup
+    kernel it replaced (WG_LEAN=0) restate the same arithmetic: their outputs must be bitwise equal,
+    including a batch whose last wave is only partly filled."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    outs = {}
+    for tag, env in (("lean", {}), ("barrier", {"WG_LEAN": "0"})):
+        path = str(tmp_path / f"{tag}.npz")
+        subprocess.run([sys.executable, os.path.join(here, "kernel_variant_run.py"), path],
+                       env=dict(os.environ, **env), check=True, timeout=300)
+        outs[tag] = np.load(path)
+    a, b = outs["lean"], outs["barrier"]
+    assert sorted(a.files) == sorted(b.files)
+    for k in a.files:
+        x, y = a[k], b[k]
+        assert x.shape == y.shape, k
+        assert np.array_equal(x.view(np.uint8), y.view(np.uint8)), k

@@ -58,11 +58,11 @@ constexpr int MAXT = 256;               // __launch_bounds__: workgroups are 64.
 // Diagnostic build only (-DWG_STAMPS): thread 0 of each workgroup records s_memrealtime (100 MHz) at
 // phase boundaries into g_stamps[block][8]; read back with wg_debug_stamps().  Never in the product.
 #ifdef WG_STAMPS
-__device__ unsigned long long g_stamps[65536 * 8];
+__device__ unsigned long long g_stamps[65536 * 16];
 #define STAMP(k)                                                                                    \
     do {                                                                                            \
         if (threadIdx.x == 0 && blockIdx.x < 65536)                                                 \
-            g_stamps[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();                      \
+            g_stamps[blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memrealtime();                      \
     } while (0)
 #else
 #define STAMP(k) do {} while (0)
@@ -345,6 +345,7 @@ __device__ __forceinline__ void mass_step(const KParams &kp, const double *st, c
     const double ym = 1.0 / md;      // one IEEE division per mass; every /m below is exact from it
     const float ymf = (float)ym;     // = RN32(1/m)
     ax = 0.f; ay = 0.f; az = 0.f;
+    STAMP(10);
     // Both ends of an edge see the same spring term t and damping force df with opposite signs; the
     // divisions are odd functions (RN is sign-symmetric), so the quotient is formed once and its sign
     // flipped by one XOR: -(t/m) == (-t)/m exactly, a + (-d) == a - d.
@@ -390,6 +391,7 @@ __device__ __forceinline__ void mass_step(const KParams &kp, const double *st, c
                 asm volatile("" : "+v"(A.t0), "+v"(A.t1), "+v"(A.t2), "+v"(A.f0), "+v"(A.f1), "+v"(A.f2), "+v"(ea), "+v"(eb));
             }
         }
+        STAMP(7);
         const bool bad = !(__builtin_isfinite(ax) && __builtin_isfinite(ay) && __builtin_isfinite(az));
         if (__builtin_expect(bad, 0)) {
             ax = 0.f; ay = 0.f; az = 0.f;
@@ -652,6 +654,7 @@ __global__ __launch_bounds__(MAXT) void walker_step_kernel(
             bool hit;
             mass_step(kp, s.t, s.df, s_inc16 + 2 * lb, lb, s0, (WG_ABLATE & 2) ? min(s1, s0 + 1) : s1, mf,
                       s.pos + 3 * lp, s.vel + 3 * lp, px, py, pz, vx, vy, vz, ax, ay, az, hit);
+            STAMP(8);
             if (b.contact) b.contact[P0 + lp] = (uint8_t)hit;
             s.pos[3 * lp] = px; s.pos[3 * lp + 1] = py; s.pos[3 * lp + 2] = pz;
             s.vel[3 * lp] = vx; s.vel[3 * lp + 1] = vy; s.vel[3 * lp + 2] = vz;
@@ -698,6 +701,7 @@ __global__ __launch_bounds__(MAXT) void walker_step_kernel(
         const float ksum = pw_sum_lanes(ke, gbase, M, lane), psum = pw_sum_lanes(pe, gbase, M, lane);
         const unsigned long long gmask = (M == 64) ? ~0ull : (((1ull << M) - 1ull) << (gbase & 63));
         // the collision penalty counts contacts of the NEW state (optimized_env.py:200 runs after run1)
+        STAMP(9);
         const unsigned long long hb = __ballot(is_mass && (py - kp.ground < 0.f));
         const unsigned long long sb = __ballot(is_mass && nv < 0.1f);
         const int hits = __popcll(hb & gmask);
@@ -1075,6 +1079,278 @@ __global__ __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(4, 8))) vo
 #undef WG_LANE_ROLES
 }
 
+// ------------------------------------------------------------------ lean wave-independent kernel
+// Uniform batches with M | 64 (4 <= M <= 64): one mass per lane, 64/M walkers per wave and NO
+// workgroup barrier.  Each wave owns a private LDS slice and runs its own load -> act -> springs ->
+// masses -> outputs sequence, so the four waves of a workgroup (and the workgroups sharing a CU) drift
+// apart and overlap one another's memory and compute phases instead of meeting at __syncthreads
+// (the phase lock measured on walker_step_kernel).  Same arithmetic as
+// walker_step_kernel, op for op; the only change is the spring's 1/dist (see rcp64_nr).
+struct LeanGeo {
+    int wpw;                                  // walkers per wave (64 / M)
+    int wpb;                                  // waves per workgroup
+    int lgM;                                  // log2(M)
+    int slice;                                // LDS bytes per wave
+    int off_df, off_inc, off_x;               // byte offsets in the slice (spring terms / obs tile at 0)
+    float invK, invA;
+};
+
+// LDS hand-off between lanes of ONE wave: a wave's LDS operations execute in order, so a compiler
+// barrier (wavefront-scope fences around the wave barrier) is all the ordering needed.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// 1/d for a double d = (double)cur, cur a normal float: v_rcp_f64 and two Newton steps, within about
+// one ulp of 1/d (not necessarily RN64(1/d)).  That suffices for the Markstein correction in
+// ddiv_fast / fdiv_fast to return the correctly rounded quotient of the spring: a quotient X/cur of two
+// 24-bit floats lies at least 2^-78 (relative) from every double rounding midpoint and 2^-49 from every
+// float one, while the corrected value is within ~2^-100 of X/cur (tests/test_exact_division.py runs
+// the same construction on the host).
+__device__ __forceinline__ double rcp64_nr(double d) {
+    double y = __builtin_amdgcn_rcp(d);
+    double e = __builtin_fma(-d, y, 1.0);
+    y = __builtin_fma(y, e, y);
+    e = __builtin_fma(-d, y, 1.0);
+    return __builtin_fma(y, e, y);
+}
+
+// Gather a float from another lane of the wave (ds_bpermute: LDS crossbar, no LDS allocation).  Executed
+// by every lane (convergent): a lane that is inactive as a SOURCE would read back as 0.
+__device__ __forceinline__ float lane_gather(float v, int src_byte) {
+    return __int_as_float(__builtin_amdgcn_ds_bpermute(src_byte, __float_as_int(v)));
+}
+
+// Spring term and damping force of one edge from its endpoints' state (gathered from the mass lanes):
+// spring_edge's arithmetic with the cheaper reciprocal (identical results; cold path unchanged).
+__device__ __forceinline__ void spring_edge_regs(const EdgeRec &e, int le, float x, float pix, float piy, float piz,
+                                                 float pjx, float pjy, float pjz, float vix, float viy, float viz,
+                                                 float vjx, float vjy, float vjz, double *st, float *sdf,
+                                                 int spring_mode) {
+    const float cur = np_norm3(pix - pjx, piy - pjy, piz - pjz);   // engine.py:86
+    const float dx = cur - x;                                       // engine.py:96
+    const float r0 = pjx - pix, r1 = pjy - piy, r2 = pjz - piz;     // other.pos - self.pos
+    double dist = (double)cur;                                      // engine.py:73
+    if (CONFIG_R > dist) dist = CONFIG_R;                           // max(distance, r)
+    const double yc = rcp64_nr(dist);
+    const float fsz = (spring_mode == 1 || !(dx < 0.f && edge_string(e.ij))) ? (-dx) * e.k : 0.f;  // :97-100
+    const float nf = -fsz;                                                                           // :75
+    const float ycf = (float)yc;
+    float d0 = fdiv_fast(r0, cur, ycf), d1 = fdiv_fast(r1, cur, ycf), d2 = fdiv_fast(r2, cur, ycf);
+    double t0, t1, t2;
+    if (spring_mode == 1) {
+        t0 = (double)(fsz * d0); t1 = (double)(fsz * d1); t2 = (double)(fsz * d2);
+    } else {
+        t0 = ddiv_fast((double)(nf * r0), dist, yc);
+        t1 = ddiv_fast((double)(nf * r1), dist, yc);
+        t2 = ddiv_fast((double)(nf * r2), dist, yc);
+    }
+    const bool fast_ok = cur > 0.f && (double)cur == dist && __builtin_isfinite(d0) && __builtin_isfinite(d1) &&
+                         __builtin_isfinite(d2) && __builtin_isfinite(t0) && __builtin_isfinite(t1) &&
+                         __builtin_isfinite(t2);
+    if (__builtin_expect(!fast_ok, 0)) {
+        d0 = r0; d1 = r1; d2 = r2;
+        if (cur > 0.f) { d0 = r0 / cur; d1 = r1 / cur; d2 = r2 / cur; }
+        if (spring_mode == 1) {
+            t0 = (double)(fsz * d0); t1 = (double)(fsz * d1); t2 = (double)(fsz * d2);
+        } else {
+            t0 = (double)(nf * r0) / dist; t1 = (double)(nf * r1) / dist; t2 = (double)(nf * r2) / dist;
+        }
+    }
+    st[3 * le] = t0; st[3 * le + 1] = t1; st[3 * le + 2] = t2;
+    const float dk = np_dot3(vix - vjx, viy - vjy, viz - vjz, d0, d1, d2);  // optimized_walker.py:102-103
+    const float dkc = dk * e.c;                                               // :104
+    sdf[3 * le] = dkc * d0; sdf[3 * le + 1] = dkc * d1; sdf[3 * le + 2] = dkc * d2;
+}
+
+template <bool IN3D, int NE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void walker_step_lean(wg_batch b, KParams kp, const float *__restrict__ action,
+                                                        int action_cols, int action_stride, wg_outputs o, LeanGeo lg) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int M = b.M, K = b.K, A = b.A;
+    const int w0 = (blockIdx.x * lg.wpb + wv) * lg.wpw;
+    if (w0 >= b.N) return;
+    const int nw = min(lg.wpw, b.N - w0);
+    char *sl = smem + wv * lg.slice;
+    double *s_t = reinterpret_cast<double *>(sl);
+    float *s_df = reinterpret_cast<float *>(sl + lg.off_df);
+    uint32_t *s_inc = reinterpret_cast<uint32_t *>(sl + lg.off_inc);
+    float *s_x = reinterpret_cast<float *>(sl + lg.off_x);
+    const int nP = nw * M, nE = nw * K, nU = nw * A;
+    const size_t P0 = (size_t)w0 * M, E0 = (size_t)w0 * K, U0 = (size_t)w0 * A;
+    const int wl = lane >> lg.lgM, q = lane & (M - 1);
+    const bool is_mass = lane < nP;
+    STAMP(0);
+
+    // ================= every global load of the wave's walkers, issued back to back =================
+    // this lane's mass: pos / vel stay in registers (the springs gather them with ds_bpermute)
+    float p3[3] = {0.f, 0.f, 0.f}, v3[3] = {0.f, 0.f, 0.f};
+    if (is_mass) {
+        const float *gp = b.pos + 3 * (P0 + lane), *gv = b.vel + 3 * (P0 + lane);
+        p3[0] = gp[0]; p3[1] = gp[1]; p3[2] = gp[2];
+        v3[0] = gv[0]; v3[1] = gv[1]; v3[2] = gv[2];
+    }
+    EdgeRec er[NE];
+    uint32_t gi[NE];
+    const uint32_t *incw = reinterpret_cast<const uint32_t *>(b.inc) + E0;   // 2 u16 entries per word
+#pragma unroll
+    for (int it = 0; it < NE; it++) {
+        const int le = lane + 64 * it;
+        if (le < nE) { er[it] = load_edge(b.edges, E0 + le); gi[it] = incw[le]; }
+    }
+    float mf = 0.f;
+    int io0 = 0, io1 = 0, wsteps = 0;
+    if (is_mass) {
+        mf = b.mass[P0 + lane];
+        const uint16_t *io = b.inc_off + (size_t)(w0 + wl) * (M + 1) + q;
+        io0 = io[0]; io1 = io[1];
+        if (q == 0) wsteps = b.steps[w0 + wl];
+    }
+    const bool is_mus = lane < nU;
+    const int mu_wl = A > 0 ? fdiv(lane, A, lg.invA) : 0, mu_ua = lane - mu_wl * A;
+    const bool acts = action != nullptr && is_mus && mu_ua < action_cols;
+    float x = 0.f, lo = 0.f, hi = 0.f, stp = 0.f, a = 0.f;
+    if (is_mus) {
+        x = b.muscle_x[U0 + lane];
+        if (acts) {
+            const float2 bd = reinterpret_cast<const float2 *>(b.muscle_bounds)[U0 + lane];
+            lo = bd.x; hi = bd.y;
+            if (kp.action_mode == 1) stp = b.muscle_stride[U0 + lane];
+            a = action[(size_t)(w0 + mu_wl) * action_stride + mu_ua];
+        }
+    }
+
+    // ================= stage the incidence lists in LDS; act (gym/optimized_walker.py:27-43,164-172)
+#pragma unroll
+    for (int it = 0; it < NE; it++)
+        if (lane + 64 * it < nE) s_inc[lane + 64 * it] = gi[it];
+    if (acts) {
+        x = (kp.action_mode == 1) ? ((a != 0.f) ? x + stp : x - stp) : x + a;
+        if (lo > x) x = lo;     // Python max(x, originx*minl)
+        if (hi < x) x = hi;     // Python min(x, originx*maxl)
+        b.muscle_x[U0 + lane] = x;
+    }
+    if (is_mus) s_x[lane] = x;
+    wave_sync();
+    STAMP(1);
+
+    // ================= springs: gym/engine.py:78-102 + gym/optimized_walker.py:92-106 =================
+#pragma unroll
+    for (int it = 0; it < NE; it++) {
+        const int le = lane + 64 * it;
+        if (64 * it >= nE) break;                          // wave-uniform
+        const EdgeRec &e = er[it];
+        const int ewl = fdiv(le, K, lg.invK), ew = le - ewl * K;
+        // endpoint state from the mass lanes: every lane takes part (inactive sources read as 0)
+        const int bi = (ewl * M + edge_i(e.ij)) << 2, bj = (ewl * M + edge_j(e.ij)) << 2;
+        const float pix = lane_gather(p3[0], bi), piy = lane_gather(p3[1], bi), piz = lane_gather(p3[2], bi);
+        const float pjx = lane_gather(p3[0], bj), pjy = lane_gather(p3[1], bj), pjz = lane_gather(p3[2], bj);
+        const float vix = lane_gather(v3[0], bi), viy = lane_gather(v3[1], bi), viz = lane_gather(v3[2], bi);
+        const float vjx = lane_gather(v3[0], bj), vjy = lane_gather(v3[1], bj), vjz = lane_gather(v3[2], bj);
+        if (le < nE)
+            spring_edge_regs(e, le, (ew < A) ? s_x[ewl * A + ew] : e.rest, pix, piy, piz, pjx, pjy, pjz, vix, viy,
+                             viz, vjx, vjy, vjz, s_t, s_df, kp.spring_mode);
+    }
+    wave_sync();
+    STAMP(2);
+
+    // ================= masses: ordered accumulation, env forces, Point.run1 =================
+    float px = 0.f, py = 0.f, pz = 0.f, vx = 0.f, vy = 0.f, vz = 0.f, ax = 0.f, ay = 0.f, az = 0.f;
+    float nv = 0.f, ke = 0.f, pe = 0.f;
+    bool hit = false;
+    if (is_mass) {
+        const int lb = wl * K;
+        mass_step(kp, s_t, s_df, reinterpret_cast<const uint16_t *>(s_inc) + 2 * lb, lb, io0, io1, mf,
+                  p3, v3, px, py, pz, vx, vy, vz, ax, ay, az, hit);
+        nv = np_norm3(vx, vy, vz);
+        ke = mf * (nv * nv);   // numpy's float32 ** 2 is libm powf: may differ by 1 ulp
+        pe = (float)((double)mf * kp.g) * (py - kp.ground);
+    }
+    STAMP(8);
+
+    // ================= per-walker reductions (wave shuffles) + outputs (gym/optimized_env.py:189-248)
+    const int gbase = lane & ~(M - 1);
+    float sx, sy, sz;
+    seq_sum3_lanes(px, py, pz, gbase, M, sx, sy, sz);
+    const float ysum = pw_sum_lanes(py, gbase, M, lane), vsum = pw_sum_lanes(nv, gbase, M, lane);
+    const float ksum = pw_sum_lanes(ke, gbase, M, lane), psum = pw_sum_lanes(pe, gbase, M, lane);
+    const unsigned long long gmask = (M == 64) ? ~0ull : (((1ull << M) - 1ull) << gbase);
+    const unsigned long long hb = __ballot(is_mass && (py - kp.ground < 0.f));   // contacts after run1 (:200)
+    const unsigned long long sb = __ballot(is_mass && nv < 0.1f);
+    const float fM = (float)M;
+    const float midx = sx / fM, midy = sy / fM, midz = sz / fM;
+    STAMP(9);
+    if (is_mass) {
+        float *gpo = b.pos + 3 * (P0 + lane), *gvo = b.vel + 3 * (P0 + lane), *gao = b.acc + 3 * (P0 + lane);
+        gpo[0] = px; gpo[1] = py; gpo[2] = pz;
+        gvo[0] = vx; gvo[1] = vy; gvo[2] = vz;
+        gao[0] = ax; gao[1] = ay; gao[2] = az;
+        if (b.contact) b.contact[P0 + lane] = (uint8_t)hit;
+        if (q == 0) {
+            const size_t wg = (size_t)(w0 + wl);
+            const int steps = wsteps + 1;
+            b.steps[wg] = steps;
+            const float cy = ysum / fM;
+            if (o.reward) {
+                const float vpen = (-(vsum / fM)) * 0.1f;
+                o.reward[wg] = (cy + vpen) + (float)(-(double)__popcll(hb & gmask) * 0.5);
+            }
+            if (o.done) {
+                int done = steps >= kp.max_steps;
+                if (!done && cy < kp.done_y) done = 1;
+                if (!done && steps > 100) done = (sb & gmask) == gmask;
+                o.done[wg] = (uint8_t)done;
+            }
+            if (o.centroid) { o.centroid[3 * wg] = midx; o.centroid[3 * wg + 1] = midy; o.centroid[3 * wg + 2] = midz; }
+            if (o.energy) o.energy[wg] = 0.5f * ksum + psum;
+        }
+    }
+    STAMP(3);
+
+    // ================= observation rows: Creature.getstat (gym/optimized_walker.py:129-162) =========
+    if (o.obs) {
+        constexpr int d = IN3D ? 3 : 2, per = 3 * d;
+        const int stride = o.obs_stride, nmid = kp.conmid ? 3 : 0;
+        float *tile = reinterpret_cast<float *>(s_t);
+        wave_sync();                      // every lane is done reading the spring terms
+        if (is_mass) {
+            float *row = tile + wl * stride + per * q;
+            const float pm[3] = {px, py, pz}, vm[3] = {vx, vy, vz}, am[3] = {ax, ay, az};
+            const float mm[3] = {midx, midy, midz};
+#pragma unroll
+            for (int c = 0; c < d; c++) {
+                row[c] = kp.midform ? (pm[c] - mm[c]) * kp.pk : pm[c] * kp.pk;
+                row[d + c] = vm[c] * kp.vk;
+                row[2 * d + c] = am[c] * kp.ak;
+            }
+            if (q == 0) {
+                float *wrow = tile + wl * stride;
+                if (nmid) {
+                    wrow[per * M] = kp.midform ? midx : 0.f; wrow[per * M + 1] = kp.midform ? midy : 0.f;
+                    wrow[per * M + 2] = kp.midform ? midz : 0.f;
+                }
+                for (int r = per * M + nmid + A; r < stride; r++) wrow[r] = 0.f;
+            }
+        }
+        if (is_mus) tile[mu_wl * stride + per * M + nmid + mu_ua] = x * kp.mk;
+        wave_sync();
+        STAMP(5);
+        float *ob = o.obs + (size_t)w0 * stride;
+        const int n = nw * stride;
+        if (((((uintptr_t)ob) & 15) == 0) && (n & 3) == 0) {
+            const float4 *s4 = reinterpret_cast<const float4 *>(tile);
+            float4 *d4 = reinterpret_cast<float4 *>(ob);
+            for (int i = lane; i < (n >> 2); i += 64) d4[i] = s4[i];
+        } else {
+            for (int i = lane; i < n; i += 64) ob[i] = tile[i];
+        }
+    }
+    STAMP(6);
+}
+
 // reset: v += noise (x, y, z if in3d), steps = 0 (PhysicsEnv.reset, gym/optimized_env.py:53-68)
 __global__ void walker_reset_kernel(wg_batch b, const float *__restrict__ noise, const uint8_t *__restrict__ mask,
                                     int in3d) {
@@ -1182,7 +1458,8 @@ template <bool STEP, bool RAGGED, bool IN3D, int PWD, bool SHFL>
 int launch(const wg_batch *b, const KParams &kp, const float *action, int cols, int astride,
            const wg_outputs &o, const int32_t *plan, int blocks, const Geo &g, hipStream_t stream) {
     if (g.lds > LDS_LIMIT) return fail(WG_ERANGE, "workgroup needs %d B of LDS (> 160 KiB)", g.lds);
-    hipLaunchKernelGGL((walker_step_kernel<STEP, RAGGED, IN3D, PWD, SHFL>), dim3(blocks), dim3(g.threads), g.lds, stream,
+    static const int lds_extra = [] { const char *e = getenv("WG_DEBUG_LDS_EXTRA"); return e ? atoi(e) : 0; }();  // experiments only
+    hipLaunchKernelGGL((walker_step_kernel<STEP, RAGGED, IN3D, PWD, SHFL>), dim3(blocks), dim3(g.threads), g.lds + lds_extra, stream,
                        *b, kp, action, cols, astride, o, plan, g);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(WG_EHIP, "launch failed: %s", hipGetErrorString(e));
@@ -1268,6 +1545,59 @@ int launch_stream(const wg_batch *b, const KParams &kp, bool in3d, const float *
     return 0;
 }
 
+// ---- lean kernel selection: uniform batch, M | 64 with M >= 4, the wave's edges in <= 8 register
+// passes, its muscles in one pass, and a workgroup LDS footprint that keeps >= 2 workgroups per CU.
+// WG_LEAN=0 selects the barrier kernels instead (A/B runs).
+bool lean_enabled() {
+    static const int m = [] { const char *e = getenv("WG_LEAN"); return e && *e ? atoi(e) : 1; }();
+    return m != 0;
+}
+
+bool lean_geo(const wg_batch *b, int obs_stride, LeanGeo *out) {
+    const int M = b->M;
+    if (b->ragged || M < 4 || M > 64 || (64 % M) != 0 || b->K < 1 || !lean_enabled() || (WG_ABLATE & 128)) return false;
+    LeanGeo g{};
+    g.wpw = 64 / M;
+    g.lgM = 0;
+    while ((1 << g.lgM) < M) g.lgM++;
+    if ((g.wpw * b->K + 63) / 64 > 8 || g.wpw * b->A > 64) return false;
+    const int tb = align16(std::max(g.wpw * b->K * 24, g.wpw * std::max(0, obs_stride) * 4));
+    g.off_df = tb;
+    g.off_inc = g.off_df + align16(g.wpw * b->K * 12);
+    g.off_x = g.off_inc + align16(g.wpw * b->K * 4);
+    g.slice = g.off_x + align16(std::max(1, g.wpw * b->A) * 4);
+    if (4 * g.slice > 80 * 1024) return false;
+    g.invK = 1.f / (float)b->K;
+    g.invA = 1.f / (float)std::max(1, b->A);
+    static const int wpb = [] { const char *e = getenv("WG_LEAN_WAVES"); return e && *e ? atoi(e) : 4; }();  // experiments
+    g.wpb = (wpb == 1 || wpb == 2) ? wpb : 4;
+    *out = g;
+    return true;
+}
+
+int launch_lean(const wg_batch *b, const KParams &kp, bool in3d, const float *a, int cols, int astride,
+                const wg_outputs &o, const LeanGeo &g, hipStream_t st) {
+    const int blocks = (b->N + g.wpb * g.wpw - 1) / (g.wpb * g.wpw);
+    const int ne = (g.wpw * b->K + 63) / 64;
+    const int lds = g.wpb * g.slice;
+#define WG_LAUNCH_LEAN(D3, NE_) \
+    hipLaunchKernelGGL((walker_step_lean<D3, NE_>), dim3(blocks), dim3(64 * g.wpb), lds, st, *b, kp, a, cols, astride, o, g)
+#define WG_LEAN_NE(D3)                                                         \
+    do {                                                                       \
+        if (ne <= 1) WG_LAUNCH_LEAN(D3, 1);                                    \
+        else if (ne == 2) WG_LAUNCH_LEAN(D3, 2);                               \
+        else if (ne == 3) WG_LAUNCH_LEAN(D3, 3);                               \
+        else if (ne == 4) WG_LAUNCH_LEAN(D3, 4);                               \
+        else WG_LAUNCH_LEAN(D3, 8);                                            \
+    } while (0)
+    if (in3d) WG_LEAN_NE(true); else WG_LEAN_NE(false);
+#undef WG_LEAN_NE
+#undef WG_LAUNCH_LEAN
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(WG_EHIP, "launch failed: %s", hipGetErrorString(e));
+    return 0;
+}
+
 template <bool STEP>
 int dispatch(const wg_batch *b, const KParams &kp, bool in3d, const float *a, int cols, int astride,
              const wg_outputs &o, const int32_t *plan, int blocks, const Geo &g, hipStream_t st) {
@@ -1292,6 +1622,8 @@ int run(const wg_batch *b, const wg_params *p, const float *action, int32_t cols
     const Geo g = b->ragged ? ragged_geo(b) : uniform_geo(b, out.obs ? out.obs_stride : 0);
     if (g.W > g.threads) return fail(WG_ERANGE, "more than %d walkers per workgroup", g.threads);
     const int blocks = b->ragged ? plan_blocks : (b->N + g.W - 1) / g.W;
+    LeanGeo lg{};
+    const bool use_lean = step && lean_geo(b, out.obs ? out.obs_stride : 0, &lg);
     for (int s = 0; s < n_steps; s++) {
         wg_outputs os = out;
         if (os.obs) os.obs += s * os.obs_step;
@@ -1300,6 +1632,11 @@ int run(const wg_batch *b, const wg_params *p, const float *action, int32_t cols
         if (os.energy) os.energy += s * os.out_step;
         if (os.centroid) os.centroid += 3 * s * os.out_step;
         const float *a = action ? action + s * astep : nullptr;
+        if (step && use_lean) {
+            rc = launch_lean(b, kp, p->in3d != 0, a, cols, astride, os, lg, stream);
+            if (rc) return rc;
+            continue;
+        }
         if (step && stream_ok(b, g)) {
             rc = launch_stream(b, kp, p->in3d != 0, a, cols, astride, os, g, stream);
             if (rc) return rc;
@@ -1368,7 +1705,7 @@ int wg_plan_ragged(const int32_t *mass_off, const int32_t *edge_off, const int32
 // diagnostic builds: copy n block stamp records (8 x u64 each) to host memory; -1 otherwise
 int wg_debug_stamps(unsigned long long *host, int n) {
 #ifdef WG_STAMPS
-    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), (size_t)n * 8 * sizeof(unsigned long long), 0,
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), (size_t)n * 16 * sizeof(unsigned long long), 0,
                             hipMemcpyDeviceToHost) != hipSuccess)
         return WG_EHIP;
     return 0;
@@ -1382,6 +1719,14 @@ int wg_launch_geometry(const wg_batch *b, wg_launch_info *info) {
     int rc = validate(b);
     if (rc) return rc;
     if (!info) return fail(WG_EINVAL, "null info");
+    LeanGeo lg{};
+    if (lean_geo(b, 0, &lg)) {   // the step kernel of uniform M | 64 batches (the obs tile may widen the slice)
+        info->threads = 64 * lg.wpb;
+        info->walkers_per_block = lg.wpb * lg.wpw;
+        info->blocks = (b->N + lg.wpb * lg.wpw - 1) / (lg.wpb * lg.wpw);
+        info->lds_bytes = lg.wpb * lg.slice;
+        return 0;
+    }
     const Geo g = b->ragged ? ragged_geo(b) : uniform_geo(b, 0);
     info->threads = g.threads;
     info->walkers_per_block = g.W;

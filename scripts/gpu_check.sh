@@ -17,7 +17,6 @@ step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider -
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py --steps 300 --warmup 30
 step rocprof_trace 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 200 --warmup 20 --no-cpu-baseline
-if [ -n "$WG_AB" ]; then
-  step bench_k0 600 env WG_STREAM=0 python bench.py --steps 300 --warmup 30 --no-cpu-baseline
-  step bench_k2 600 env WG_STREAM=2 python bench.py --steps 300 --warmup 30 --no-cpu-baseline
+if [ -n "$WG_AB" ]; then  # A/B: barrier kernel vs lean
+  step bench_barrier 600 env WG_LEAN=0 python bench.py --steps 300 --warmup 30 --no-cpu-baseline
 fi

@@ -340,7 +340,7 @@ __device__ __forceinline__ void mass_step(const KParams &kp, const double *st, c
                                           const uint16_t *inc, int lb, int s0, int s1, float mf,
                                           const float *p3, const float *v3, float &px, float &py, float &pz,
                                           float &vx, float &vy, float &vz, float &ax, float &ay, float &az,
-                                          bool &hit) {
+                                          bool &hit, int spring_mode) {
     const double md = (double)mf;
     const double ym = 1.0 / md;      // one IEEE division per mass; every /m below is exact from it
     const float ymf = (float)ym;     // = RN32(1/m)
@@ -349,7 +349,7 @@ __device__ __forceinline__ void mass_step(const KParams &kp, const double *st, c
     // Both ends of an edge see the same spring term t and damping force df with opposite signs; the
     // divisions are odd functions (RN is sign-symmetric), so the quotient is formed once and its sign
     // flipped by one XOR: -(t/m) == (-t)/m exactly, a + (-d) == a - d.
-    if (kp.spring_mode == 1) {
+    if (spring_mode == 1) {
         for (int r = s0; r < s1; r++) {
             const int ent = inc[r];
             const int le = lb + (ent >> 1);
@@ -653,7 +653,7 @@ __global__ __launch_bounds__(MAXT) void walker_step_kernel(
             const double md = (double)mf;
             bool hit;
             mass_step(kp, s.t, s.df, s_inc16 + 2 * lb, lb, s0, (WG_ABLATE & 2) ? min(s1, s0 + 1) : s1, mf,
-                      s.pos + 3 * lp, s.vel + 3 * lp, px, py, pz, vx, vy, vz, ax, ay, az, hit);
+                      s.pos + 3 * lp, s.vel + 3 * lp, px, py, pz, vx, vy, vz, ax, ay, az, hit, kp.spring_mode);
             STAMP(8);
             if (b.contact) b.contact[P0 + lp] = (uint8_t)hit;
             s.pos[3 * lp] = px; s.pos[3 * lp + 1] = py; s.pos[3 * lp + 2] = pz;
@@ -802,7 +802,7 @@ __global__ __launch_bounds__(MAXT) void walker_step_kernel(
     if (o.obs && !(WG_ABLATE & 16)) {
         constexpr int d = IN3D ? 3 : 2, per = 3 * d;
         const int stride = o.obs_stride;
-        float *ob = o.obs + (size_t)w0 * stride;
+        float *ob = o.obs + (uint32_t)w0 * (uint32_t)stride;
         // uniform batches assemble the rows in LDS (aliasing the dead spring-term region) and stream
         // them out as one contiguous 16-B-store block; ragged batches write rows directly.
         float *tile = RAGGED ? nullptr : reinterpret_cast<float *>(s.t);
@@ -995,7 +995,8 @@ __global__ __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(4, 8))) vo
         if (is_mass) {
             const int lb = my_wl * K;
             mass_step(kp, s.t, s.df, reinterpret_cast<const uint16_t *>(s.inc) + 2 * lb, lb, (int)(io & 0xffffu),
-                      (int)(io >> 16), mf, s.pos + 3 * tid, s.vel + 3 * tid, px, py, pz, vx, vy, vz, ax, ay, az, hit);
+                      (int)(io >> 16), mf, s.pos + 3 * tid, s.vel + 3 * tid, px, py, pz, vx, vy, vz, ax, ay, az, hit,
+                      kp.spring_mode);
             nv = np_norm3(vx, vy, vz);
             ke = mf * (nv * nv);     // numpy's float32 ** 2 is libm powf: may differ by 1 ulp
             pe_ = (float)((double)mf * kp.g) * (py - kp.ground);
@@ -1089,6 +1090,7 @@ __global__ __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(4, 8))) vo
 struct LeanGeo {
     int wpw;                                  // walkers per wave (64 / M)
     int wpb;                                  // waves per workgroup
+    int persist;                              // grid sized to the resident capacity, waves loop over tiles
     int lgM;                                  // log2(M)
     int slice;                                // LDS bytes per wave
     int off_df, off_inc, off_x;               // byte offsets in the slice (spring terms / obs tile at 0)
@@ -1165,31 +1167,31 @@ __device__ __forceinline__ void spring_edge_regs(const EdgeRec &e, int le, float
     sdf[3 * le] = dkc * d0; sdf[3 * le + 1] = dkc * d1; sdf[3 * le + 2] = dkc * d2;
 }
 
+// One wave's tile: walkers [tile*wpw, tile*wpw + wpw) of the batch, LDS slice `sl`.
 template <bool IN3D, int NE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void walker_step_lean(wg_batch b, KParams kp, const float *__restrict__ action,
-                                                        int action_cols, int action_stride, wg_outputs o, LeanGeo lg) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+__device__ __forceinline__ void lean_tile(const wg_batch &b, const KParams &kp, const float *__restrict__ action,
+                                          int action_cols, int action_stride, const wg_outputs &o, const LeanGeo &lg,
+                                          char *sl, int tile, int lane) {
     const int M = b.M, K = b.K, A = b.A;
-    const int w0 = (blockIdx.x * lg.wpb + wv) * lg.wpw;
-    if (w0 >= b.N) return;
+    const int w0 = tile * lg.wpw;
     const int nw = min(lg.wpw, b.N - w0);
-    char *sl = smem + wv * lg.slice;
     double *s_t = reinterpret_cast<double *>(sl);
     float *s_df = reinterpret_cast<float *>(sl + lg.off_df);
     uint32_t *s_inc = reinterpret_cast<uint32_t *>(sl + lg.off_inc);
     float *s_x = reinterpret_cast<float *>(sl + lg.off_x);
     const int nP = nw * M, nE = nw * K, nU = nw * A;
-    const size_t P0 = (size_t)w0 * M, E0 = (size_t)w0 * K, U0 = (size_t)w0 * A;
+    // 32-bit element offsets (host-checked to fit)
+    const uint32_t P0 = (uint32_t)w0 * M, E0 = (uint32_t)w0 * K, U0 = (uint32_t)w0 * A;
     const int wl = lane >> lg.lgM, q = lane & (M - 1);
     const bool is_mass = lane < nP;
+    const uint32_t pl = P0 + lane;        // this lane's mass
     STAMP(0);
 
     // ================= every global load of the wave's walkers, issued back to back =================
     // this lane's mass: pos / vel stay in registers (the springs gather them with ds_bpermute)
     float p3[3] = {0.f, 0.f, 0.f}, v3[3] = {0.f, 0.f, 0.f};
     if (is_mass) {
-        const float *gp = b.pos + 3 * (P0 + lane), *gv = b.vel + 3 * (P0 + lane);
+        const float *gp = b.pos + 3 * (size_t)pl, *gv = b.vel + 3 * (size_t)pl;
         p3[0] = gp[0]; p3[1] = gp[1]; p3[2] = gp[2];
         v3[0] = gv[0]; v3[1] = gv[1]; v3[2] = gv[2];
     }
@@ -1199,27 +1201,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void w
 #pragma unroll
     for (int it = 0; it < NE; it++) {
         const int le = lane + 64 * it;
-        if (le < nE) { er[it] = load_edge(b.edges, E0 + le); gi[it] = incw[le]; }
+        if (le < nE) { er[it] = load_edge(b.edges, E0 + (uint32_t)le); gi[it] = incw[(uint32_t)le]; }
     }
     float mf = 0.f;
     int io0 = 0, io1 = 0, wsteps = 0;
     if (is_mass) {
-        mf = b.mass[P0 + lane];
-        const uint16_t *io = b.inc_off + (size_t)(w0 + wl) * (M + 1) + q;
-        io0 = io[0]; io1 = io[1];
-        if (q == 0) wsteps = b.steps[w0 + wl];
+        mf = b.mass[pl];
+        const uint32_t io = (uint32_t)(w0 + wl) * (M + 1) + q;
+        io0 = b.inc_off[io]; io1 = b.inc_off[io + 1];
+        if (q == 0) wsteps = b.steps[(uint32_t)(w0 + wl)];
     }
     const bool is_mus = lane < nU;
     const int mu_wl = A > 0 ? fdiv(lane, A, lg.invA) : 0, mu_ua = lane - mu_wl * A;
     const bool acts = action != nullptr && is_mus && mu_ua < action_cols;
     float x = 0.f, lo = 0.f, hi = 0.f, stp = 0.f, a = 0.f;
+    const uint32_t ul = U0 + lane;        // this lane's muscle
     if (is_mus) {
-        x = b.muscle_x[U0 + lane];
+        x = b.muscle_x[ul];
         if (acts) {
-            const float2 bd = reinterpret_cast<const float2 *>(b.muscle_bounds)[U0 + lane];
+            const float2 bd = reinterpret_cast<const float2 *>(b.muscle_bounds)[ul];
             lo = bd.x; hi = bd.y;
-            if (kp.action_mode == 1) stp = b.muscle_stride[U0 + lane];
-            a = action[(size_t)(w0 + mu_wl) * action_stride + mu_ua];
+            if (kp.action_mode == 1) stp = b.muscle_stride[ul];
+            a = action[(uint32_t)(w0 + mu_wl) * (uint32_t)action_stride + (uint32_t)mu_ua];
         }
     }
 
@@ -1231,7 +1234,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void w
         x = (kp.action_mode == 1) ? ((a != 0.f) ? x + stp : x - stp) : x + a;
         if (lo > x) x = lo;     // Python max(x, originx*minl)
         if (hi < x) x = hi;     // Python min(x, originx*maxl)
-        b.muscle_x[U0 + lane] = x;
+        b.muscle_x[ul] = x;
     }
     if (is_mus) s_x[lane] = x;
     wave_sync();
@@ -1252,7 +1255,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void w
         const float vjx = lane_gather(v3[0], bj), vjy = lane_gather(v3[1], bj), vjz = lane_gather(v3[2], bj);
         if (le < nE)
             spring_edge_regs(e, le, (ew < A) ? s_x[ewl * A + ew] : e.rest, pix, piy, piz, pjx, pjy, pjz, vix, viy,
-                             viz, vjx, vjy, vjz, s_t, s_df, kp.spring_mode);
+                             viz, vjx, vjy, vjz, s_t, s_df, 0);   // lean path: spring_mode 0 only
     }
     wave_sync();
     STAMP(2);
@@ -1264,7 +1267,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void w
     if (is_mass) {
         const int lb = wl * K;
         mass_step(kp, s_t, s_df, reinterpret_cast<const uint16_t *>(s_inc) + 2 * lb, lb, io0, io1, mf,
-                  p3, v3, px, py, pz, vx, vy, vz, ax, ay, az, hit);
+                  p3, v3, px, py, pz, vx, vy, vz, ax, ay, az, hit, 0);
         nv = np_norm3(vx, vy, vz);
         ke = mf * (nv * nv);   // numpy's float32 ** 2 is libm powf: may differ by 1 ulp
         pe = (float)((double)mf * kp.g) * (py - kp.ground);
@@ -1284,13 +1287,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void w
     const float midx = sx / fM, midy = sy / fM, midz = sz / fM;
     STAMP(9);
     if (is_mass) {
-        float *gpo = b.pos + 3 * (P0 + lane), *gvo = b.vel + 3 * (P0 + lane), *gao = b.acc + 3 * (P0 + lane);
+        float *gpo = b.pos + 3 * (size_t)pl, *gvo = b.vel + 3 * (size_t)pl, *gao = b.acc + 3 * (size_t)pl;
         gpo[0] = px; gpo[1] = py; gpo[2] = pz;
         gvo[0] = vx; gvo[1] = vy; gvo[2] = vz;
         gao[0] = ax; gao[1] = ay; gao[2] = az;
-        if (b.contact) b.contact[P0 + lane] = (uint8_t)hit;
+        if (b.contact) b.contact[pl] = (uint8_t)hit;
         if (q == 0) {
-            const size_t wg = (size_t)(w0 + wl);
+            const uint32_t wg = (uint32_t)(w0 + wl);
             const int steps = wsteps + 1;
             b.steps[wg] = steps;
             const float cy = ysum / fM;
@@ -1314,10 +1317,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void w
     if (o.obs) {
         constexpr int d = IN3D ? 3 : 2, per = 3 * d;
         const int stride = o.obs_stride, nmid = kp.conmid ? 3 : 0;
-        float *tile = reinterpret_cast<float *>(s_t);
+        float *otile = reinterpret_cast<float *>(s_t);
         wave_sync();                      // every lane is done reading the spring terms
         if (is_mass) {
-            float *row = tile + wl * stride + per * q;
+            float *row = otile + wl * stride + per * q;
             const float pm[3] = {px, py, pz}, vm[3] = {vx, vy, vz}, am[3] = {ax, ay, az};
             const float mm[3] = {midx, midy, midz};
 #pragma unroll
@@ -1327,7 +1330,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void w
                 row[2 * d + c] = am[c] * kp.ak;
             }
             if (q == 0) {
-                float *wrow = tile + wl * stride;
+                float *wrow = otile + wl * stride;
                 if (nmid) {
                     wrow[per * M] = kp.midform ? midx : 0.f; wrow[per * M + 1] = kp.midform ? midy : 0.f;
                     wrow[per * M + 2] = kp.midform ? midz : 0.f;
@@ -1335,20 +1338,42 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void w
                 for (int r = per * M + nmid + A; r < stride; r++) wrow[r] = 0.f;
             }
         }
-        if (is_mus) tile[mu_wl * stride + per * M + nmid + mu_ua] = x * kp.mk;
+        if (is_mus) otile[mu_wl * stride + per * M + nmid + mu_ua] = x * kp.mk;
         wave_sync();
         STAMP(5);
-        float *ob = o.obs + (size_t)w0 * stride;
+        float *ob = o.obs + (uint32_t)w0 * (uint32_t)stride;
         const int n = nw * stride;
         if (((((uintptr_t)ob) & 15) == 0) && (n & 3) == 0) {
-            const float4 *s4 = reinterpret_cast<const float4 *>(tile);
+            const float4 *s4 = reinterpret_cast<const float4 *>(otile);
             float4 *d4 = reinterpret_cast<float4 *>(ob);
             for (int i = lane; i < (n >> 2); i += 64) d4[i] = s4[i];
         } else {
-            for (int i = lane; i < n; i += 64) ob[i] = tile[i];
+            for (int i = lane; i < n; i += 64) ob[i] = otile[i];
         }
     }
     STAMP(6);
+}
+
+template <bool IN3D, int NE, bool PERSIST>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void walker_step_lean(
+    wg_batch b, KParams kp, const float *__restrict__ action, int action_cols, int action_stride, wg_outputs o,
+    LeanGeo lg) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    char *sl = smem + wv * lg.slice;
+    int tile = blockIdx.x * lg.wpb + wv;
+    if (!PERSIST) {
+        if (tile * lg.wpw < b.N) lean_tile<IN3D, NE>(b, kp, action, action_cols, action_stride, o, lg, sl, tile, lane);
+        return;
+    }
+    // persistent grid: a wave's tiles are tile, tile + (waves in the grid), ...
+    const int stride = gridDim.x * lg.wpb;
+    for (; tile * lg.wpw < b.N; tile += stride) {
+        int t_opaque = tile, l_opaque = lane;
+        asm volatile("" : "+v"(l_opaque), "+v"(t_opaque));   // keep per-tile index math inside the loop
+        lean_tile<IN3D, NE>(b, kp, action, action_cols, action_stride, o, lg, sl, t_opaque, l_opaque);
+        wave_sync();                                          // the next tile reuses the slice
+    }
 }
 
 // reset: v += noise (x, y, z if in3d), steps = 0 (PhysicsEnv.reset, gym/optimized_env.py:53-68)
@@ -1553,9 +1578,14 @@ bool lean_enabled() {
     return m != 0;
 }
 
-bool lean_geo(const wg_batch *b, int obs_stride, LeanGeo *out) {
+bool lean_geo(const wg_batch *b, int obs_stride, LeanGeo *out, int spring_mode = 0) {
     const int M = b->M;
     if (b->ragged || M < 4 || M > 64 || (64 % M) != 0 || b->K < 1 || !lean_enabled() || (WG_ABLATE & 128)) return false;
+    if (spring_mode != 0) return false;          // the G2-compat element runs on the workgroup kernel
+    // 32-bit element offsets inside the kernel
+    if ((int64_t)b->N * b->M * 3 >= (1ll << 31) || (int64_t)b->N * b->K * 4 >= (1ll << 31) ||
+        (int64_t)b->N * std::max(obs_stride, 1) >= (1ll << 31))
+        return false;
     LeanGeo g{};
     g.wpw = 64 / M;
     g.lgM = 0;
@@ -1571,17 +1601,33 @@ bool lean_geo(const wg_batch *b, int obs_stride, LeanGeo *out) {
     g.invA = 1.f / (float)std::max(1, b->A);
     static const int wpb = [] { const char *e = getenv("WG_LEAN_WAVES"); return e && *e ? atoi(e) : 4; }();  // experiments
     g.wpb = (wpb == 1 || wpb == 2) ? wpb : 4;
+    static const int persist = [] { const char *e = getenv("WG_LEAN_PERSIST"); return e && *e ? atoi(e) : 0; }();
+    g.persist = persist;
     *out = g;
     return true;
 }
 
 int launch_lean(const wg_batch *b, const KParams &kp, bool in3d, const float *a, int cols, int astride,
                 const wg_outputs &o, const LeanGeo &g, hipStream_t st) {
-    const int blocks = (b->N + g.wpb * g.wpw - 1) / (g.wpb * g.wpw);
+    int blocks = (b->N + g.wpb * g.wpw - 1) / (g.wpb * g.wpw);
     const int ne = (g.wpw * b->K + 63) / 64;
     const int lds = g.wpb * g.slice;
-#define WG_LAUNCH_LEAN(D3, NE_) \
-    hipLaunchKernelGGL((walker_step_lean<D3, NE_>), dim3(blocks), dim3(64 * g.wpb), lds, st, *b, kp, a, cols, astride, o, g)
+    if (g.persist) {
+        int cus = 256, dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 256;
+        const int per_cu = std::max(1, std::min((160 * 1024 - 4096) / lds, 24 / g.wpb));   // LDS share, 6 waves/SIMD
+        blocks = std::min(blocks, per_cu * cus);
+    }
+#define WG_LAUNCH_LEAN(D3, NE_)                                                                                  \
+    do {                                                                                                         \
+        if (g.persist)                                                                                           \
+            hipLaunchKernelGGL((walker_step_lean<D3, NE_, true>), dim3(blocks), dim3(64 * g.wpb), lds, st, *b, kp, a, \
+                               cols, astride, o, g);                                                             \
+        else                                                                                                     \
+            hipLaunchKernelGGL((walker_step_lean<D3, NE_, false>), dim3(blocks), dim3(64 * g.wpb), lds, st, *b, kp,   \
+                               a, cols, astride, o, g);                                                          \
+    } while (0)
 #define WG_LEAN_NE(D3)                                                         \
     do {                                                                       \
         if (ne <= 1) WG_LAUNCH_LEAN(D3, 1);                                    \
@@ -1623,7 +1669,7 @@ int run(const wg_batch *b, const wg_params *p, const float *action, int32_t cols
     if (g.W > g.threads) return fail(WG_ERANGE, "more than %d walkers per workgroup", g.threads);
     const int blocks = b->ragged ? plan_blocks : (b->N + g.W - 1) / g.W;
     LeanGeo lg{};
-    const bool use_lean = step && lean_geo(b, out.obs ? out.obs_stride : 0, &lg);
+    const bool use_lean = step && lean_geo(b, out.obs ? out.obs_stride : 0, &lg, p->spring_mode);
     for (int s = 0; s < n_steps; s++) {
         wg_outputs os = out;
         if (os.obs) os.obs += s * os.obs_step;

@@ -26,7 +26,7 @@
 #include <omp.h>
 #endif
 
-#define ORC_ABI 1
+#define ORC_ABI 2
 int orc_abi_version(void) { return ORC_ABI; }
 
 /* Config.r (gym/engine.py:9, gym/optimized_engine.py:7): the distance clamp, a Python float. */
@@ -193,9 +193,20 @@ static void walker_step(const orc_batch *b, const orc_params *p, int w, const fl
             a[2] = add_f32(a[2], (-v[2]) * ff, mf);
         }
         if (b->contact) b->contact[q] = (uint8_t)hit;   /* replaces color/r (optimized_env.py:155-175) */
-        /* 5. Point.run1 (gym/engine.py:168-178): v += a*t; pos += v*t; old_a = a; a = 0. */
-        v[0] = v[0] + a[0] * dt; v[1] = v[1] + a[1] * dt; v[2] = v[2] + a[2] * dt;
-        x[0] = x[0] + v[0] * dt; x[1] = x[1] + v[1] * dt; x[2] = x[2] + v[2] * dt;
+        /* DingPoint (gym/optimized_engine.py:404-416): forced() is a no-op, so every force above left
+         * its a at the zeros() of step 2; the env then integrates it with the base Point.run1. */
+        if (b->pinned && b->pinned[q]) a[0] = a[1] = a[2] = 0.f;
+        if (p->integrator == 2) {
+            /* 5'. Point.run2 (gym/engine.py:180-190): pos += v*t + 0.5*a*t**2; v += a*t.  numpy order:
+             *     (v*t) + ((0.5*a) * float32(t**2)), t**2 a Python float. */
+            const float dt2 = (float)(p->dt * p->dt);
+            for (int c = 0; c < 3; c++) x[c] = x[c] + (v[c] * dt + (0.5f * a[c]) * dt2);
+            for (int c = 0; c < 3; c++) v[c] = v[c] + a[c] * dt;
+        } else {
+            /* 5. Point.run1 (gym/engine.py:168-178): v += a*t; pos += v*t; old_a = a; a = 0. */
+            v[0] = v[0] + a[0] * dt; v[1] = v[1] + a[1] * dt; v[2] = v[2] + a[2] * dt;
+            x[0] = x[0] + v[0] * dt; x[1] = x[1] + v[1] * dt; x[2] = x[2] + v[2] * dt;
+        }
         /* acc now holds old_a (the acceleration used in this step) */
     }
     b->steps[w] += 1;                                    /* PhysicsEnv.step, optimized_env.py:84 */

@@ -18,6 +18,7 @@ typedef struct orc_params {
     int32_t in3d, max_steps, midform, conmid;
     int32_t spring_mode;   /* 0 = engine.py resilience + G2 damping; 1 = G2 optimized_walker as written */
     int32_t action_mode;   /* 0 = Muscle.act (continuous); 1 = Muscle.actdisp (discrete) */
+    int32_t integrator;    /* 0/1 = Point.run1 (gym/engine.py:168-178); 2 = Point.run2 (:180-190) */
 } orc_params;
 
 typedef struct orc_batch {
@@ -32,6 +33,7 @@ typedef struct orc_batch {
     const float *minl, *maxl, *stride; /* [U] */
     int32_t *steps;                  /* [N] */
     uint8_t *contact;                /* [P] (may be NULL) */
+    const uint8_t *pinned;           /* [P] 1 = DingPoint, forced() a no-op (may be NULL) */
 } orc_batch;
 
 typedef struct orc_out {

@@ -17,7 +17,10 @@ mechanical fixes SURVEY.md §8(c) lists (the reference's env loop cannot run as 
                   k=0 spring adds +/-0 to the accelerations, which is a no-op).
 Everything else is the reference's code, called directly:
   * action          ``optimized_walker.Muscle.act/actdisp/regulation`` via ``Creature.act`` (:27-43,164-172)
-  * integrator      ``gym.engine.Point.run1`` (gym/engine.py:168-178)
+  * integrator      ``gym.engine.Point.run1`` (gym/engine.py:168-178), or ``Point.run2`` (:180-190)
+                    for the run2 scenario
+  * pinned masses   ``optimized_engine.DingPoint`` objects (gym/optimized_engine.py:404-416: forced() is a
+                    no-op), integrated by the same base ``Point.run1`` the envs call
   * observation     ``optimized_walker.Creature.getstat`` (:129-162)
   * reward/done/info ``optimized_env.PhysicsEnv._get_reward/_is_done/_get_info/_calculate_energy``
                     (gym/optimized_env.py:189-248), bound to a data shim
@@ -76,7 +79,7 @@ class Spec:
     """A batch in the flat CSR layout used by the oracle and the GPU path."""
 
     def __init__(self, m, pos, vel, mass_off, ei, ej, rest, k, c, flags, edge_off, n_muscles,
-                 minl, maxl, stride, acc=None):
+                 minl, maxl, stride, acc=None, pinned=None, mx=None):
         self.m = np.asarray(m, np.float32)
         self.pos = np.asarray(pos, np.float32).reshape(-1, 3)
         self.vel = np.asarray(vel, np.float32).reshape(-1, 3)
@@ -89,6 +92,7 @@ class Spec:
         self.n_muscles = np.asarray(n_muscles, np.int32)
         self.minl = np.asarray(minl, np.float32); self.maxl = np.asarray(maxl, np.float32)
         self.stride = np.asarray(stride, np.float32)
+        self.pinned = np.zeros(len(self.m), np.uint8) if pinned is None else np.asarray(pinned, np.uint8)
 
     @property
     def N(self):
@@ -102,6 +106,8 @@ class Spec:
         for key in ("m", "pos", "vel", "acc", "mass_off", "ei", "ej", "rest", "k", "c", "flags",
                     "edge_off", "n_muscles", "minl", "maxl", "stride"):
             d[prefix + key] = getattr(self, key)
+        if self.pinned.any():
+            d[prefix + "pinned"] = self.pinned
         return d
 
 
@@ -127,10 +133,10 @@ def spec_from_creatures(creatures, point_index):
 
 
 PARAM_KEYS = ("g", "dampk", "ground", "groundk", "grounddamp", "friction", "dt", "in3d", "max_steps",
-              "pk", "vk", "ak", "mk", "midform", "conmid", "spring_mode")
+              "pk", "vk", "ak", "mk", "midform", "conmid", "spring_mode", "integrator")
 DEFAULT_PARAMS = dict(g=100.0, dampk=0.0, ground=0.0, groundk=1000.0, grounddamp=100.0, friction=100.0,
                       dt=0.01, in3d=1, max_steps=1000, pk=1.0, vk=1.0, ak=1.0, mk=1.0, midform=1,
-                      conmid=0, spring_mode=0)
+                      conmid=0, spring_mode=0, integrator=1)
 
 
 class RefRun:
@@ -185,7 +191,10 @@ class RefRun:
                     p.forced(np.array([-p.v[0] * friction_force, 0, -p.v[2] * friction_force], dtype=f32))
                 else:
                     p.color = "black"; p.r = 1
-        E.Point.run1(P["dt"])                      # gym/engine.py:168-178
+        if P["integrator"] == 2:
+            E.Point.run2(P["dt"])                  # gym/engine.py:180-190
+        else:
+            E.Point.run1(P["dt"])                  # gym/engine.py:168-178
 
     def act(self, actions):
         for w, cr in enumerate(self.cr):
@@ -263,7 +272,8 @@ def pad_obs(obs_list):
 
 
 def params_array(p):
-    return {"param_" + k: np.array(p[k]) for k in PARAM_KEYS}
+    # integrator is recorded only where it is not the default, so the older fixtures stay byte-stable
+    return {"param_" + k: np.array(p[k]) for k in PARAM_KEYS if k != "integrator" or p[k] != 1}
 
 
 # --------------------------------------------------------------------------- creature builders
@@ -273,7 +283,15 @@ def creatures_from_spec(E, OW, spec: Spec):
     mo = spec.muscle_off()
     for w in range(spec.N):
         a, b = spec.mass_off[w], spec.mass_off[w + 1]
-        phys = [E.Point(float(spec.m[q]), spec.pos[q].copy(), spec.vel[q].copy()) for q in range(a, b)]
+        phys = []
+        for q in range(a, b):
+            if spec.pinned[q]:
+                # the reference's DingPoint(m, p, v) (gym/optimized_engine.py:404-410), run by E.Point.run1
+                p = sys.modules["optimized_engine"].DingPoint(float(spec.m[q]), spec.pos[q].copy(), spec.vel[q].copy())
+                E.Point.points.append(p)
+            else:
+                p = E.Point(float(spec.m[q]), spec.pos[q].copy(), spec.vel[q].copy())
+            phys.append(p)
         for q, p in zip(range(a, b), phys):
             p.old_a = spec.acc[q].copy()
         e0, e1 = spec.edge_off[w], spec.edge_off[w + 1]
@@ -311,6 +329,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
     ap.add_argument("--out", default=HERE)
+    ap.add_argument("--only", nargs="*", default=None, help="write only these fixtures (others still run)")
     args = ap.parse_args()
     E, OW, OE = load_reference(args.ref)
     rng = np.random.default_rng(20251212)
@@ -329,6 +348,8 @@ def main():
         blob.update(outs)
         if extra:
             blob.update(extra)
+        if args.only is not None and name not in args.only:
+            return
         path = os.path.join(args.out, name + ".npz")
         np.savez_compressed(path, **blob)
         written.append((name, os.path.getsize(path)))
@@ -437,6 +458,43 @@ def main():
     acts = rng.uniform(-1, 1, (60, 1, 2)).astype(f32)
     run = RefRun(E, OW, OE, crs, dict(in3d=1, spring_mode=1))
     save("g2_compat", run, spec, 60, acts)
+
+    rng2 = np.random.default_rng(20260101)     # scenarios added later draw from their own stream
+
+    # K. pinned masses (DingPoint): the G1 balance3 topology (gym/walker.py:212-223, Phy(m, v, p)
+    #    argument order as its DingPoint(m, v, p) at gym/engine.py:570) and canonical walkers with two
+    #    pinned masses each; reset noise moves the pinned masses (a stays 0), 60 steps.
+    fresh()
+    b3 = dict(m=[1, 1, 1, 0.1], pos=[[-50, 100, 0], [50, 100, 0], [0, 0, 0], [0, 100, 0]], vel=np.zeros((4, 3)),
+              mass_off=[0, 4], ei=[0, 1, 0, 0, 1], ej=[2, 2, 1, 3, 3], k=[1000, 1000, 1000, 20000, 20000],
+              c=[20] * 5, flags=[0] * 5, edge_off=[0, 5], n_muscles=[2], minl=[0.1, 0.1], maxl=[1.5, 1.5],
+              stride=[2, 2], pinned=[0, 0, 1, 0])
+    b3["rest"] = [float(np.linalg.norm(np.asarray(b3["pos"][i], f32) - np.asarray(b3["pos"][j], f32)))
+                  for i, j in zip(b3["ei"], b3["ej"])]
+    cw = canonical_walkers(3, seed=21)
+    cw["pinned"] = np.zeros(48, np.uint8); cw["pinned"][[0, 5, 16 + 3, 16 + 12, 32 + 15, 32 + 7]] = 1
+    for name, sp, in3d, A in (("pinned_balance3", b3, 0, 2), ("pinned_canonical", cw, 1, 8)):
+        fresh()
+        spec = Spec(**sp)
+        crs = creatures_from_spec(E, OW, spec)
+        noise = rng2.normal(0, 0.5, (spec.mass_off[-1], 3)).astype(f32)
+        acts = rng2.uniform(-1, 1, (60, spec.N, A)).astype(f32)
+        run = RefRun(E, OW, OE, crs, dict(in3d=in3d))
+        save(name, run, spec, 60, acts, noise=noise)
+
+    # L. Point.run2 integrator (gym/engine.py:180-190) on canonical walkers and Balance-v0, 60 steps.
+    fresh()
+    spec = Spec(**canonical_walkers(3, seed=23))
+    crs = creatures_from_spec(E, OW, spec)
+    acts = rng2.uniform(-1, 1, (60, 3, 8)).astype(f32)
+    run = RefRun(E, OW, OE, crs, dict(in3d=1, integrator=2))
+    save("run2_canonical", run, spec, 60, acts)
+    fresh()
+    crs = reference_builders(E, OW, "balance", 2)
+    spec = spec_from_creatures(crs, None)
+    acts = rng2.uniform(-1, 1, (60, 2, 2)).astype(f32)
+    run = RefRun(E, OW, OE, crs, dict(in3d=0, integrator=2))
+    save("run2_balance", run, spec, 60, acts)
 
     for name, size in written:
         print(f"{name:16s} {size:9d} B")

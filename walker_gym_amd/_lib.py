@@ -13,7 +13,7 @@ import threading
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libwalker_hip.so"
 LIB_PATH = os.path.join(HERE, LIB_NAME)
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 WG_EINVAL, WG_ERANGE, WG_EHIP = -1, -2, -3
 
@@ -23,7 +23,8 @@ _vp = C.c_void_p
 class WgParams(C.Structure):
     _fields_ = [(n, C.c_double) for n in ("g", "dampk", "ground", "groundk", "grounddamp", "friction", "dt",
                                            "pk", "vk", "ak", "mk")] + \
-               [(n, C.c_int32) for n in ("in3d", "max_steps", "midform", "conmid", "spring_mode", "action_mode")]
+               [(n, C.c_int32) for n in ("in3d", "max_steps", "midform", "conmid", "spring_mode", "action_mode",
+                                         "integrator")]
 
 
 class WgBatch(C.Structure):
@@ -34,7 +35,7 @@ class WgBatch(C.Structure):
                 ("edges", _vp),
                 ("inc", _vp), ("inc_off", _vp),
                 ("muscle_x", _vp), ("muscle_bounds", _vp), ("muscle_stride", _vp),
-                ("steps", _vp), ("contact", _vp)]
+                ("steps", _vp), ("contact", _vp), ("pinned", _vp)]
 
 
 class WgOutputs(C.Structure):

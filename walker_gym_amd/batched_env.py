@@ -43,11 +43,17 @@ class EnvParams:
     conmid: bool = False
     spring_mode: int = 0          # 0: engine.py resilience + damping; 1: G2 optimized_walker as written
     action_mode: int = 0          # 0: Muscle.act; 1: Muscle.actdisp
+    integrator: int = 1           # 1: Point.run1 (what the envs call); 2: Point.run2 (gym/engine.py:180-190)
 
     def to_struct(self) -> _lib.WgParams:
         d = asdict(self)
+        if d["integrator"] in ("run1", "run2"):
+            d["integrator"] = int(d["integrator"][-1])
+        if int(d["integrator"]) not in (0, 1, 2):
+            raise ValueError("integrator must be 1 ('run1') or 2 ('run2')")
         return _lib.WgParams(**{k: (int(v) if k in ("in3d", "max_steps", "midform", "conmid", "spring_mode",
-                                                    "action_mode") else float(v)) for k, v in d.items()})
+                                                    "action_mode", "integrator") else float(v))
+                                for k, v in d.items()})
 
 
 class BatchedPhysicsEnv:

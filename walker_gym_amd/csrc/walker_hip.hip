@@ -72,8 +72,10 @@ __device__ unsigned long long g_stamps[65536 * 16];
 struct KParams {
     float neg_g, neg_dampk, ground, neg_groundk, neg_grounddamp, friction, dt;
     float pk, vk, ak, mk, done_y;
+    float dt2;      // run2: float32(t ** 2), t**2 a Python float (double) cast where numpy casts it
     double g;
     int max_steps, midform, conmid, spring_mode, action_mode;
+    int integrator; // 2: Point.run2, otherwise Point.run1
     int stagger;    // diagnostics (WG_STAGGER): blocks with blockIdx % 4 == k idle k*stagger*64 cycles first
 };
 
@@ -340,7 +342,7 @@ __device__ __forceinline__ void mass_step(const KParams &kp, const double *st, c
                                           const uint16_t *inc, int lb, int s0, int s1, float mf,
                                           const float *p3, const float *v3, float &px, float &py, float &pz,
                                           float &vx, float &vy, float &vz, float &ax, float &ay, float &az,
-                                          bool &hit, int spring_mode) {
+                                          bool &hit, int spring_mode, bool pinned) {
     const double md = (double)mf;
     const double ym = 1.0 / md;      // one IEEE division per mass; every /m below is exact from it
     const float ymf = (float)ym;     // = RN32(1/m)
@@ -427,8 +429,17 @@ __device__ __forceinline__ void mass_step(const KParams &kp, const double *st, c
         const float ff = fabsf(deep) * kp.friction;                  // :168
         ax = ax + fdiv_mk((-vx) * ff, mf, ymf); ay = ay + zm; az = az + fdiv_mk((-vz) * ff, mf, ymf);
     }
-    vx = vx + ax * kp.dt; vy = vy + ay * kp.dt; vz = vz + az * kp.dt;   // Point.run1
-    px = px + vx * kp.dt; py = py + vy * kp.dt; pz = pz + vz * kp.dt;
+    if (pinned) { ax = 0.f; ay = 0.f; az = 0.f; }   // DingPoint.forced is a no-op: a stays zeros()
+    if (kp.integrator == 2) {
+        // Point.run2 (gym/engine.py:184-187): pos += v*t + 0.5*a*t**2 (numpy: (v*t) + ((0.5*a)*f32(t**2))), v += a*t
+        px = px + (vx * kp.dt + (0.5f * ax) * kp.dt2);
+        py = py + (vy * kp.dt + (0.5f * ay) * kp.dt2);
+        pz = pz + (vz * kp.dt + (0.5f * az) * kp.dt2);
+        vx = vx + ax * kp.dt; vy = vy + ay * kp.dt; vz = vz + az * kp.dt;
+    } else {
+        vx = vx + ax * kp.dt; vy = vy + ay * kp.dt; vz = vz + az * kp.dt;   // Point.run1
+        px = px + vx * kp.dt; py = py + vy * kp.dt; pz = pz + vz * kp.dt;
+    }
 }
 
 // ------------------------------------------------------------------ cross-lane reductions
@@ -653,7 +664,8 @@ __global__ __launch_bounds__(MAXT) void walker_step_kernel(
             const double md = (double)mf;
             bool hit;
             mass_step(kp, s.t, s.df, s_inc16 + 2 * lb, lb, s0, (WG_ABLATE & 2) ? min(s1, s0 + 1) : s1, mf,
-                      s.pos + 3 * lp, s.vel + 3 * lp, px, py, pz, vx, vy, vz, ax, ay, az, hit, kp.spring_mode);
+                      s.pos + 3 * lp, s.vel + 3 * lp, px, py, pz, vx, vy, vz, ax, ay, az, hit, kp.spring_mode,
+                      b.pinned && b.pinned[P0 + lp]);
             STAMP(8);
             if (b.contact) b.contact[P0 + lp] = (uint8_t)hit;
             s.pos[3 * lp] = px; s.pos[3 * lp + 1] = py; s.pos[3 * lp + 2] = pz;
@@ -996,7 +1008,7 @@ __global__ __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(4, 8))) vo
             const int lb = my_wl * K;
             mass_step(kp, s.t, s.df, reinterpret_cast<const uint16_t *>(s.inc) + 2 * lb, lb, (int)(io & 0xffffu),
                       (int)(io >> 16), mf, s.pos + 3 * tid, s.vel + 3 * tid, px, py, pz, vx, vy, vz, ax, ay, az, hit,
-                      kp.spring_mode);
+                      kp.spring_mode, b.pinned && b.pinned[P0 + tid]);
             nv = np_norm3(vx, vy, vz);
             ke = mf * (nv * nv);     // numpy's float32 ** 2 is libm powf: may differ by 1 ulp
             pe_ = (float)((double)mf * kp.g) * (py - kp.ground);
@@ -1205,8 +1217,10 @@ __device__ __forceinline__ void lean_tile(const wg_batch &b, const KParams &kp, 
     }
     float mf = 0.f;
     int io0 = 0, io1 = 0, wsteps = 0;
+    bool pin = false;
     if (is_mass) {
         mf = b.mass[pl];
+        if (b.pinned) pin = b.pinned[pl] != 0;
         const uint32_t io = (uint32_t)(w0 + wl) * (M + 1) + q;
         io0 = b.inc_off[io]; io1 = b.inc_off[io + 1];
         if (q == 0) wsteps = b.steps[(uint32_t)(w0 + wl)];
@@ -1267,7 +1281,7 @@ __device__ __forceinline__ void lean_tile(const wg_batch &b, const KParams &kp, 
     if (is_mass) {
         const int lb = wl * K;
         mass_step(kp, s_t, s_df, reinterpret_cast<const uint16_t *>(s_inc) + 2 * lb, lb, io0, io1, mf,
-                  p3, v3, px, py, pz, vx, vy, vz, ax, ay, az, hit, 0);
+                  p3, v3, px, py, pz, vx, vy, vz, ax, ay, az, hit, 0, pin);
         nv = np_norm3(vx, vy, vz);
         ke = mf * (nv * nv);   // numpy's float32 ** 2 is libm powf: may differ by 1 ulp
         pe = (float)((double)mf * kp.g) * (py - kp.ground);
@@ -1415,6 +1429,8 @@ KParams make_kparams(const wg_params &p) {
     k.g = p.g;
     k.max_steps = p.max_steps; k.midform = p.midform; k.conmid = p.conmid;
     k.spring_mode = p.spring_mode; k.action_mode = p.action_mode;
+    k.integrator = p.integrator;
+    k.dt2 = (float)(p.dt * p.dt);
     static const int stagger = [] { const char *e = getenv("WG_STAGGER"); return e ? atoi(e) : 0; }();
     k.stagger = stagger;
     return k;
@@ -1660,6 +1676,7 @@ int run(const wg_batch *b, const wg_params *p, const float *action, int32_t cols
     if (b->N == 0 || n_steps <= 0) return 0;
     if (action && (cols < 0 || astride < cols)) return fail(WG_EINVAL, "bad action stride");
     if (action && p->action_mode == 1 && !b->muscle_stride) return fail(WG_EINVAL, "discrete actions need muscle_stride");
+    if (p->integrator < 0 || p->integrator > 2) return fail(WG_EINVAL, "integrator must be 0/1 (run1) or 2 (run2)");
     if (action && !b->muscle_bounds) return fail(WG_EINVAL, "actions need muscle_bounds");
     if (b->ragged && (!plan || plan_blocks <= 0)) return fail(WG_EINVAL, "ragged batch needs a plan");
     wg_outputs out = o ? *o : wg_outputs{};

@@ -56,6 +56,7 @@ class DeviceBatch:
         self.muscle_stride = _to_dev(host.muscle_stride, dv)
         self.steps = _to_dev(host.steps, dv)
         self.contact = torch.zeros(self.P, dtype=torch.uint8, device=dv) if contact else None
+        self.pinned = _to_dev(host.pinned, dv) if host.pinned is not None else None
         # placeholders so that zero-size arrays still have a valid device pointer
         self._dummy = torch.zeros(16, dtype=torch.float32, device=dv)
         self.plan = None
@@ -88,7 +89,8 @@ class DeviceBatch:
             edges=self._p(self.edges),
             inc=self._p(self.inc) if self.inc is not None else None, inc_off=self._p(self.inc_off),
             muscle_x=self._p(self.muscle_x), muscle_bounds=self._p(self.muscle_bounds),
-            muscle_stride=self._p(self.muscle_stride), steps=self._p(self.steps), contact=self._p(self.contact))
+            muscle_stride=self._p(self.muscle_stride), steps=self._p(self.steps), contact=self._p(self.contact),
+            pinned=self._p(self.pinned))
 
     def launch_geometry(self) -> dict:
         info = _lib.WgLaunchInfo()

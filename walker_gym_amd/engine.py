@@ -95,8 +95,10 @@ class Point:
 
 
 class DingPoint(Point):
-    """Pinned point (gym/optimized_engine.py:404-426).  Recognised by the packer, which rejects it:
-    pinned nodes are a SURVEY §8(f) 'next' item not implemented by the kernel yet."""
+    """Pinned point (gym/optimized_engine.py:404-426).  The packer marks it in ``pinned``; the kernel
+    then skips its force accumulation (DingPoint.forced is a no-op, :412-414), so its a stays zero and
+    the env's base Point.run1 integrates it with its current velocity (DingPoint.run1 is never called
+    by the envs: gym/optimized_env.py:178 calls Point.run1)."""
 
     def __init__(self, m, p, v=None, r=None, color="black"):
         super().__init__(m, p, [0, 0, 0] if v is None else v, r, color)

@@ -48,6 +48,7 @@ class HostLayout:
     muscle_bounds: np.ndarray  # float32 [U, 2]
     muscle_stride: np.ndarray
     steps: np.ndarray
+    pinned: Optional[np.ndarray] = None   # uint8 [P]: DingPoint masses (None = no pinned mass)
     extra: Dict[str, np.ndarray] = field(default_factory=dict)
 
     @property
@@ -163,7 +164,18 @@ def pack(spec: Dict[str, np.ndarray], mx: Optional[np.ndarray] = None, steps: Op
         muscle_bounds=np.ascontiguousarray(np.stack([lo, hi], axis=1).reshape(-1, 2), f32),
         muscle_stride=np.ascontiguousarray(s["stride"], f32),
         steps=(np.zeros(N, np.int32) if steps is None else np.ascontiguousarray(steps, np.int32).copy()),
+        pinned=_pinned(spec, int(mass_off[-1])),
     )
+
+
+def _pinned(spec, P: int):
+    pin = spec.get("pinned")
+    if pin is None:
+        return None
+    pin = np.ascontiguousarray(pin, np.uint8).reshape(-1)
+    if pin.shape[0] != P:
+        raise ValueError(f"pinned has {pin.shape[0]} entries for {P} masses")
+    return (pin != 0).astype(np.uint8) if pin.any() else None
 
 
 def algorithmic_bytes_per_walker_step(M: int, K: int, A: int, obs_floats: int) -> int:

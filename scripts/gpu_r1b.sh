@@ -1,0 +1,19 @@
+#!/bin/bash
+# Session: kernel-variant bit-equality (lean / barrier / prefetch / quotient variants), in-process A/B of
+# the lean variants, lean phase ablation.  Each GPU step has its own time limit; a crash, abort or timeout
+# (rc >= 124) ends the session.
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {  # step <name> <timeout_s> <cmd...>
+  local name=$1 t=$2; shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "   rc=$rc"; tail -n 12 "gpurun_out/$name.log"
+  if [ $rc -ge 2 ] && [ $rc -ne 5 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+step variants 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v -p no:cacheprovider --timeout 400 --timeout-method thread -k variants
+step lean_ab 300 python -u scripts/lean_ab.py 4
+if [ -d build_ablate ]; then step ablate 400 python -u scripts/ablate.py run; fi

@@ -227,21 +227,30 @@ def test_rollout_equals_stepwise():
 
 
 def test_kernel_variants_agree(tmp_path):
-    """The wave-independent lean kernel (default for uniform M | 64 batches) and the workgroup
-    kernel it replaced (WG_LEAN=0) restate the same arithmetic: their outputs must be bitwise equal,
-    including a batch whose last wave is only partly filled."""
+    """The wave-independent lean kernel (default for uniform M | 64 batches), the workgroup kernel it
+    replaced (WG_LEAN=0) and the lean variants (prefetching persistent waves, end quotients formed in the
+    edge phase) restate the same arithmetic: their outputs must be bitwise equal, including a batch whose
+    last wave is only partly filled."""
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     outs = {}
-    for tag, env in (("lean", {}), ("barrier", {"WG_LEAN": "0"})):
+    variants = (("lean", {}), ("barrier", {"WG_LEAN": "0"}),
+                # persistent waves with next-tile prefetch; a small grid so every wave walks many tiles
+                ("prefetch", {"WG_LEAN_PERSIST": "2", "WG_LEAN_BLOCKS": "3"}),
+                # end quotients formed in the edge phase, one tile per wave and persistent + prefetch
+                ("quo", {"WG_LEAN_QUO": "1"}),
+                ("quo_prefetch", {"WG_LEAN_QUO": "1", "WG_LEAN_PERSIST": "2", "WG_LEAN_BLOCKS": "5"}))
+    for tag, env in variants:
         path = str(tmp_path / f"{tag}.npz")
         subprocess.run([sys.executable, os.path.join(here, "kernel_variant_run.py"), path],
                        env=dict(os.environ, **env), check=True, timeout=300)
         outs[tag] = np.load(path)
-    a, b = outs["lean"], outs["barrier"]
-    assert sorted(a.files) == sorted(b.files)
-    for k in a.files:
-        x, y = a[k], b[k]
-        assert x.shape == y.shape, k
-        assert np.array_equal(x.view(np.uint8), y.view(np.uint8)), k
+    a = outs["lean"]
+    for tag, _ in variants[1:]:
+        b = outs[tag]
+        assert sorted(a.files) == sorted(b.files), tag
+        for k in a.files:
+            x, y = a[k], b[k]
+            assert x.shape == y.shape, (tag, k)
+            assert np.array_equal(x.view(np.uint8), y.view(np.uint8)), (tag, k)

@@ -334,6 +334,41 @@ __device__ __forceinline__ void acc_f64_entry(const IncTerm &q, int ent, double 
     az = az + fxsign(fdiv_fast(q.f2, mf, ymf), sd);
 }
 
+// Env forces on one mass after its spring terms, each one Point.forced in the reference's order: gravity
+// [0,-g,0]/m, damp -dampk*v/m (gym/env.py:32-33, optimized_env.py:148-151), the ground penalty when below
+// ground (:154-172); then Point.run1 / run2 (gym/engine.py:168-190).  a (in: spring terms) becomes old_a.
+__device__ __forceinline__ void mass_tail(const KParams &kp, float mf, float ymf, const float *p3, const float *v3,
+                                          float &px, float &py, float &pz, float &vx, float &vy, float &vz,
+                                          float &ax, float &ay, float &az, bool &hit, bool pinned) {
+    vx = v3[0]; vy = v3[1]; vz = v3[2];
+    px = p3[0]; py = p3[1]; pz = p3[2];
+    const float zm = fdiv_mk(0.f, mf, ymf);   // the zero components of the env forces, divided by m
+    // gravity [0,-g,0]/m, damp -dampk*v/m  (gym/env.py:32-33, optimized_env.py:148-151)
+    ax = ax + zm; ay = ay + fdiv_mk(kp.neg_g, mf, ymf); az = az + zm;
+    ax = ax + fdiv_mk(kp.neg_dampk * vx, mf, ymf);
+    ay = ay + fdiv_mk(kp.neg_dampk * vy, mf, ymf);
+    az = az + fdiv_mk(kp.neg_dampk * vz, mf, ymf);
+    const float deep = py - kp.ground;
+    hit = deep < 0.f;                                                // optimized_env.py:154
+    if (hit) {
+        ax = ax + zm; ay = ay + fdiv_mk(kp.neg_groundk * deep, mf, ymf); az = az + zm;
+        ax = ax + zm; ay = ay + fdiv_mk(kp.neg_grounddamp * vy, mf, ymf); az = az + zm;
+        const float ff = fabsf(deep) * kp.friction;                  // :168
+        ax = ax + fdiv_mk((-vx) * ff, mf, ymf); ay = ay + zm; az = az + fdiv_mk((-vz) * ff, mf, ymf);
+    }
+    if (pinned) { ax = 0.f; ay = 0.f; az = 0.f; }   // DingPoint.forced is a no-op: a stays zeros()
+    if (kp.integrator == 2) {
+        // Point.run2 (gym/engine.py:184-187): pos += v*t + 0.5*a*t**2 (numpy: (v*t) + ((0.5*a)*f32(t**2))), v += a*t
+        px = px + (vx * kp.dt + (0.5f * ax) * kp.dt2);
+        py = py + (vy * kp.dt + (0.5f * ay) * kp.dt2);
+        pz = pz + (vz * kp.dt + (0.5f * az) * kp.dt2);
+        vx = vx + ax * kp.dt; vy = vy + ay * kp.dt; vz = vz + az * kp.dt;
+    } else {
+        vx = vx + ax * kp.dt; vy = vy + ay * kp.dt; vz = vz + az * kp.dt;   // Point.run1
+        px = px + vx * kp.dt; py = py + vy * kp.dt; pz = pz + vz * kp.dt;
+    }
+}
+
 // Mass `lp`: the ordered force accumulation over its incidence list (edge order, spring then damping
 // per edge — gym/optimized_walker.py:124-127 with gym/engine.py:65-76, 101-102), then gravity, linear
 // damping and the ground penalty (gym/env.py:31-41 / gym/optimized_env.py:146-172, each one
@@ -413,33 +448,7 @@ __device__ __forceinline__ void mass_step(const KParams &kp, const double *st, c
             }
         }
     }
-    vx = v3[0]; vy = v3[1]; vz = v3[2];
-    px = p3[0]; py = p3[1]; pz = p3[2];
-    const float zm = fdiv_mk(0.f, mf, ymf);   // the zero components of the env forces, divided by m
-    // gravity [0,-g,0]/m, damp -dampk*v/m  (gym/env.py:32-33, optimized_env.py:148-151)
-    ax = ax + zm; ay = ay + fdiv_mk(kp.neg_g, mf, ymf); az = az + zm;
-    ax = ax + fdiv_mk(kp.neg_dampk * vx, mf, ymf);
-    ay = ay + fdiv_mk(kp.neg_dampk * vy, mf, ymf);
-    az = az + fdiv_mk(kp.neg_dampk * vz, mf, ymf);
-    const float deep = py - kp.ground;
-    hit = deep < 0.f;                                                // optimized_env.py:154
-    if (hit) {
-        ax = ax + zm; ay = ay + fdiv_mk(kp.neg_groundk * deep, mf, ymf); az = az + zm;
-        ax = ax + zm; ay = ay + fdiv_mk(kp.neg_grounddamp * vy, mf, ymf); az = az + zm;
-        const float ff = fabsf(deep) * kp.friction;                  // :168
-        ax = ax + fdiv_mk((-vx) * ff, mf, ymf); ay = ay + zm; az = az + fdiv_mk((-vz) * ff, mf, ymf);
-    }
-    if (pinned) { ax = 0.f; ay = 0.f; az = 0.f; }   // DingPoint.forced is a no-op: a stays zeros()
-    if (kp.integrator == 2) {
-        // Point.run2 (gym/engine.py:184-187): pos += v*t + 0.5*a*t**2 (numpy: (v*t) + ((0.5*a)*f32(t**2))), v += a*t
-        px = px + (vx * kp.dt + (0.5f * ax) * kp.dt2);
-        py = py + (vy * kp.dt + (0.5f * ay) * kp.dt2);
-        pz = pz + (vz * kp.dt + (0.5f * az) * kp.dt2);
-        vx = vx + ax * kp.dt; vy = vy + ay * kp.dt; vz = vz + az * kp.dt;
-    } else {
-        vx = vx + ax * kp.dt; vy = vy + ay * kp.dt; vz = vz + az * kp.dt;   // Point.run1
-        px = px + vx * kp.dt; py = py + vy * kp.dt; pz = pz + vz * kp.dt;
-    }
+    mass_tail(kp, mf, ymf, p3, v3, px, py, pz, vx, vy, vz, ax, ay, az, hit, pinned);
 }
 
 // ------------------------------------------------------------------ cross-lane reductions
@@ -1102,11 +1111,14 @@ __global__ __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(4, 8))) vo
 struct LeanGeo {
     int wpw;                                  // walkers per wave (64 / M)
     int wpb;                                  // waves per workgroup
-    int persist;                              // grid sized to the resident capacity, waves loop over tiles
+    int persist;                              // 0: one tile per wave; 1: persistent waves loop over tiles;
+                                              // 2: persistent, next tile's loads in flight (walker_step_lean_pf)
+    int quo;                                  // 1: per-end quotients formed in the edge phase (lean_compute)
     int lgM;                                  // log2(M)
     int slice;                                // LDS bytes per wave
     int off_df, off_inc, off_x;               // byte offsets in the slice (spring terms / obs tile at 0)
-    float invK, invA;
+    int n2;                                   // incidence entries of a full wave tile (2 * wpw * K)
+    float invK, invA, invM;                   // invM = 1/M, exact (M | 64 is a power of two)
 };
 
 // LDS hand-off between lanes of ONE wave: a wave's LDS operations execute in order, so a compiler
@@ -1139,10 +1151,10 @@ __device__ __forceinline__ float lane_gather(float v, int src_byte) {
 
 // Spring term and damping force of one edge from its endpoints' state (gathered from the mass lanes):
 // spring_edge's arithmetic with the cheaper reciprocal (identical results; cold path unchanged).
-__device__ __forceinline__ void spring_edge_regs(const EdgeRec &e, int le, float x, float pix, float piy, float piz,
-                                                 float pjx, float pjy, float pjz, float vix, float viy, float viz,
-                                                 float vjx, float vjy, float vjz, double *st, float *sdf,
-                                                 int spring_mode) {
+__device__ __forceinline__ void spring_terms(const EdgeRec &e, float x, float pix, float piy, float piz, float pjx,
+                                             float pjy, float pjz, float vix, float viy, float viz, float vjx,
+                                             float vjy, float vjz, double &t0, double &t1, double &t2, float &g0,
+                                             float &g1, float &g2, int spring_mode) {
     const float cur = np_norm3(pix - pjx, piy - pjy, piz - pjz);   // engine.py:86
     const float dx = cur - x;                                       // engine.py:96
     const float r0 = pjx - pix, r1 = pjy - piy, r2 = pjz - piz;     // other.pos - self.pos
@@ -1153,7 +1165,6 @@ __device__ __forceinline__ void spring_edge_regs(const EdgeRec &e, int le, float
     const float nf = -fsz;                                                                           // :75
     const float ycf = (float)yc;
     float d0 = fdiv_fast(r0, cur, ycf), d1 = fdiv_fast(r1, cur, ycf), d2 = fdiv_fast(r2, cur, ycf);
-    double t0, t1, t2;
     if (spring_mode == 1) {
         t0 = (double)(fsz * d0); t1 = (double)(fsz * d1); t2 = (double)(fsz * d2);
     } else {
@@ -1173,84 +1184,176 @@ __device__ __forceinline__ void spring_edge_regs(const EdgeRec &e, int le, float
             t0 = (double)(nf * r0) / dist; t1 = (double)(nf * r1) / dist; t2 = (double)(nf * r2) / dist;
         }
     }
-    st[3 * le] = t0; st[3 * le + 1] = t1; st[3 * le + 2] = t2;
     const float dk = np_dot3(vix - vjx, viy - vjy, viz - vjz, d0, d1, d2);  // optimized_walker.py:102-103
     const float dkc = dk * e.c;                                               // :104
-    sdf[3 * le] = dkc * d0; sdf[3 * le + 1] = dkc * d1; sdf[3 * le + 2] = dkc * d2;
+    g0 = dkc * d0; g1 = dkc * d1; g2 = dkc * d2;
+}
+__device__ __forceinline__ void spring_edge_regs(const EdgeRec &e, int le, float x, float pix, float piy, float piz,
+                                                 float pjx, float pjy, float pjz, float vix, float viy, float viz,
+                                                 float vjx, float vjy, float vjz, double *st, float *sdf,
+                                                 int spring_mode) {
+    double t0, t1, t2;
+    float g0, g1, g2;
+    spring_terms(e, x, pix, piy, piz, pjx, pjy, pjz, vix, viy, viz, vjx, vjy, vjz, t0, t1, t2, g0, g1, g2, spring_mode);
+    st[3 * le] = t0; st[3 * le + 1] = t1; st[3 * le + 2] = t2;
+    sdf[3 * le] = g0; sdf[3 * le + 1] = g1; sdf[3 * le + 2] = g2;
 }
 
-// One wave's tile: walkers [tile*wpw, tile*wpw + wpw) of the batch, LDS slice `sl`.
-template <bool IN3D, int NE>
-__device__ __forceinline__ void lean_tile(const wg_batch &b, const KParams &kp, const float *__restrict__ action,
-                                          int action_cols, int action_stride, const wg_outputs &o, const LeanGeo &lg,
-                                          char *sl, int tile, int lane) {
-    const int M = b.M, K = b.K, A = b.A;
-    const int w0 = tile * lg.wpw;
-    const int nw = min(lg.wpw, b.N - w0);
-    double *s_t = reinterpret_cast<double *>(sl);
-    float *s_df = reinterpret_cast<float *>(sl + lg.off_df);
-    uint32_t *s_inc = reinterpret_cast<uint32_t *>(sl + lg.off_inc);
-    float *s_x = reinterpret_cast<float *>(sl + lg.off_x);
-    const int nP = nw * M, nE = nw * K, nU = nw * A;
-    // 32-bit element offsets (host-checked to fit)
-    const uint32_t P0 = (uint32_t)w0 * M, E0 = (uint32_t)w0 * K, U0 = (uint32_t)w0 * A;
-    const int wl = lane >> lg.lgM, q = lane & (M - 1);
-    const bool is_mass = lane < nP;
-    const uint32_t pl = P0 + lane;        // this lane's mass
-    STAMP(0);
+// ------------------------------------------------------------------ lean wave tile: loads, then compute
+// Global inputs of one wave's tile, held in registers: lean_load issues every HBM read of the tile back to
+// back, lean_compute consumes them.  walker_step_lean_pf keeps the NEXT tile's LeanIn in flight while the
+// current tile computes.
+template <int NE>
+struct LeanIn {
+    float p3[3], v3[3];          // this lane's mass: pos, vel (the springs gather them with ds_bpermute)
+    EdgeRec er[NE];              // this lane's spring record in each edge pass
+    uint32_t gi[NE];             // incidence words (two u16 entries each)
+    float mf;                    // mass
+    int io0, io1, wsteps, pin;   // incidence range; step counter (q == 0 lanes); DingPoint flag
+    float x, lo, hi, stp, a;     // this lane's muscle: Muscle.x, regulation bounds, stride, action
+};
 
-    // ================= every global load of the wave's walkers, issued back to back =================
-    // this lane's mass: pos / vel stay in registers (the springs gather them with ds_bpermute)
-    float p3[3] = {0.f, 0.f, 0.f}, v3[3] = {0.f, 0.f, 0.f};
-    if (is_mass) {
+// A wave's tile: its walker range and the lane roles in it (no memory access).
+struct LeanTile {
+    int w0, nw, nP, nE, nU, wl, q, mu_wl, mu_ua;
+    uint32_t P0, E0, U0;         // 32-bit element offsets (host-checked to fit)
+    bool is_mass, is_mus, acts;
+};
+
+__device__ __forceinline__ LeanTile lean_tile_of(const wg_batch &b, const float *action, int action_cols,
+                                                 const LeanGeo &lg, int tile, int lane) {
+    LeanTile t;
+    t.w0 = tile * lg.wpw;
+    t.nw = min(lg.wpw, b.N - t.w0);
+    t.nP = t.nw * b.M; t.nE = t.nw * b.K; t.nU = t.nw * b.A;
+    t.P0 = (uint32_t)t.w0 * b.M; t.E0 = (uint32_t)t.w0 * b.K; t.U0 = (uint32_t)t.w0 * b.A;
+    t.wl = lane >> lg.lgM; t.q = lane & (b.M - 1);
+    t.is_mass = lane < t.nP;
+    t.is_mus = lane < t.nU;
+    t.mu_wl = b.A > 0 ? fdiv(lane, b.A, lg.invA) : 0;
+    t.mu_ua = lane - t.mu_wl * b.A;
+    t.acts = action != nullptr && t.is_mus && t.mu_ua < action_cols;
+    return t;
+}
+
+// Every global load of the wave's walkers, issued back to back.
+template <int NE>
+__device__ __forceinline__ void lean_load(const wg_batch &b, const KParams &kp, const float *__restrict__ action,
+                                          int action_stride, const LeanTile &t, int lane, LeanIn<NE> &L) {
+    const uint32_t pl = t.P0 + lane;        // this lane's mass
+    L.p3[0] = 0.f; L.p3[1] = 0.f; L.p3[2] = 0.f;
+    L.v3[0] = 0.f; L.v3[1] = 0.f; L.v3[2] = 0.f;
+    if (t.is_mass) {
         const float *gp = b.pos + 3 * (size_t)pl, *gv = b.vel + 3 * (size_t)pl;
-        p3[0] = gp[0]; p3[1] = gp[1]; p3[2] = gp[2];
-        v3[0] = gv[0]; v3[1] = gv[1]; v3[2] = gv[2];
+        L.p3[0] = gp[0]; L.p3[1] = gp[1]; L.p3[2] = gp[2];
+        L.v3[0] = gv[0]; L.v3[1] = gv[1]; L.v3[2] = gv[2];
     }
-    EdgeRec er[NE];
-    uint32_t gi[NE];
-    const uint32_t *incw = reinterpret_cast<const uint32_t *>(b.inc) + E0;   // 2 u16 entries per word
+    const uint32_t *incw = reinterpret_cast<const uint32_t *>(b.inc) + t.E0;   // 2 u16 entries per word
 #pragma unroll
     for (int it = 0; it < NE; it++) {
         const int le = lane + 64 * it;
-        if (le < nE) { er[it] = load_edge(b.edges, E0 + (uint32_t)le); gi[it] = incw[(uint32_t)le]; }
+        if (le < t.nE) { L.er[it] = load_edge(b.edges, t.E0 + (uint32_t)le); L.gi[it] = incw[(uint32_t)le]; }
     }
-    float mf = 0.f;
-    int io0 = 0, io1 = 0, wsteps = 0;
-    bool pin = false;
-    if (is_mass) {
-        mf = b.mass[pl];
-        if (b.pinned) pin = b.pinned[pl] != 0;
-        const uint32_t io = (uint32_t)(w0 + wl) * (M + 1) + q;
-        io0 = b.inc_off[io]; io1 = b.inc_off[io + 1];
-        if (q == 0) wsteps = b.steps[(uint32_t)(w0 + wl)];
+    L.mf = 0.f; L.io0 = 0; L.io1 = 0; L.wsteps = 0; L.pin = 0;
+    if (t.is_mass) {
+        L.mf = b.mass[pl];
+        if (b.pinned) L.pin = b.pinned[pl];
+        const uint32_t io = (uint32_t)(t.w0 + t.wl) * (b.M + 1) + t.q;
+        L.io0 = b.inc_off[io]; L.io1 = b.inc_off[io + 1];
+        if (t.q == 0) L.wsteps = b.steps[(uint32_t)(t.w0 + t.wl)];
     }
-    const bool is_mus = lane < nU;
-    const int mu_wl = A > 0 ? fdiv(lane, A, lg.invA) : 0, mu_ua = lane - mu_wl * A;
-    const bool acts = action != nullptr && is_mus && mu_ua < action_cols;
-    float x = 0.f, lo = 0.f, hi = 0.f, stp = 0.f, a = 0.f;
-    const uint32_t ul = U0 + lane;        // this lane's muscle
-    if (is_mus) {
-        x = b.muscle_x[ul];
-        if (acts) {
+    L.x = 0.f; L.lo = 0.f; L.hi = 0.f; L.stp = 0.f; L.a = 0.f;
+    const uint32_t ul = t.U0 + lane;        // this lane's muscle
+    if (t.is_mus) {
+        L.x = b.muscle_x[ul];
+        if (t.acts) {
             const float2 bd = reinterpret_cast<const float2 *>(b.muscle_bounds)[ul];
-            lo = bd.x; hi = bd.y;
-            if (kp.action_mode == 1) stp = b.muscle_stride[ul];
-            a = action[(uint32_t)(w0 + mu_wl) * (uint32_t)action_stride + (uint32_t)mu_ua];
+            L.lo = bd.x; L.hi = bd.y;
+            if (kp.action_mode == 1) L.stp = b.muscle_stride[ul];
+            L.a = action[(uint32_t)(t.w0 + t.mu_wl) * (uint32_t)action_stride + (uint32_t)t.mu_ua];
         }
     }
+}
 
-    // ================= stage the incidence lists in LDS; act (gym/optimized_walker.py:27-43,164-172)
+// double gathered from another lane (two ds_bpermute), all lanes taking part
+__device__ __forceinline__ double lane_gather_d(double v, int src_byte) {
+    return __hiloint2double(__builtin_amdgcn_ds_bpermute(src_byte, __double2hiint(v)),
+                            __builtin_amdgcn_ds_bpermute(src_byte, __double2loint(v)));
+}
+
+// QUO: one end's share of an edge, formed by the edge lane: the spring quotient t/m (float64, Point.forced
+// with a float64 force, gym/engine.py:67,75) and the damping quotient df/m (float32, gym/optimized_walker.py:
+// 105-106), the end's sign already applied to t and df (division is sign-symmetric), stored at the end's
+// slot in its mass's incidence list.  The unguarded Markstein quotients equal the IEEE ones whenever they
+// are finite (mass_step); otherwise the IEEE divisions are redone here (cold).
+__device__ __forceinline__ void end_terms(double t0, double t1, double t2, float f0, float f1, float f2, float mf,
+                                          double ym, double *sq, float *sqd, int slot, int n2) {
+    const double md = (double)mf;
+    const float ymf = (float)ym;
+    double q0 = ddiv_fast(t0, md, ym), q1 = ddiv_fast(t1, md, ym), q2 = ddiv_fast(t2, md, ym);
+    float c0 = fdiv_fast(f0, mf, ymf), c1 = fdiv_fast(f1, mf, ymf), c2 = fdiv_fast(f2, mf, ymf);
+    if (__builtin_expect(!(__builtin_isfinite(q0 + q1 + q2) && __builtin_isfinite(c0 + c1 + c2)), 0)) {
+        q0 = t0 / md; q1 = t1 / md; q2 = t2 / md;
+        c0 = f0 / mf; c1 = f1 / mf; c2 = f2 / mf;
+    }
+    sq[slot] = q0; sq[n2 + slot] = q1; sq[2 * n2 + slot] = q2;
+    sqd[slot] = c0; sqd[n2 + slot] = c1; sqd[2 * n2 + slot] = c2;
+}
+
+// One wave's tile after its loads.  QUO = false: the edge lanes leave the spring term t and the damping
+// force df per edge in LDS, the mass lanes divide by m while walking their incidence lists (mass_step).
+// QUO = true: the edge lanes also form both ends' quotients (end_terms, edge-parallel: 83 % lane use for the
+// canonical walker) and the mass lanes only add them in order (the list walk runs to the wave's longest
+// list, ~2x the mean, so moving the divisions out of it removes most of its cost).  Same bits either way.
+template <bool IN3D, int NE, bool QUO>
+__device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &kp, const wg_outputs &o,
+                                             const LeanGeo &lg, char *sl, const LeanTile &t, int lane,
+                                             const LeanIn<NE> &L) {
+    const int M = b.M, K = b.K, A = b.A;
+    const int w0 = t.w0, nw = t.nw, nE = t.nE;
+    const int wl = t.wl, q = t.q, mu_wl = t.mu_wl, mu_ua = t.mu_ua;
+    const bool is_mass = t.is_mass, is_mus = t.is_mus, acts = t.acts;
+    const uint32_t pl = t.P0 + lane, ul = t.U0 + lane;   // this lane's mass / muscle
+    // slice: QUO = false: t (f64 x3 per edge) | df (f32 x3) | incidence words | muscle x
+    //        QUO = true:  q (f64, 3 planes of n2 slots) | df/m (f32, 3 planes) | slot of each (edge, end) | x
+    // the obs tile aliases the first region once the masses are done
+    double *s_t = reinterpret_cast<double *>(sl);
+    float *s_df = reinterpret_cast<float *>(sl + lg.off_df);
+    uint32_t *s_inc = reinterpret_cast<uint32_t *>(sl + lg.off_inc);
+    uint16_t *s_slot = reinterpret_cast<uint16_t *>(sl + lg.off_inc);
+    float *s_x = reinterpret_cast<float *>(sl + lg.off_x);
+    const float mf = L.mf;
+    const bool pin = L.pin != 0;
+    STAMP(0);
+
+    // ================= incidence lists into LDS; act (gym/optimized_walker.py:27-43,164-172)
+    if (QUO) {
+        // incidence word le holds entries 2le, 2le+1 of the tile's list, both of walker le / K: record for each
+        // (edge << 1 | end) its position in its mass's list, the slot its quotients go to
 #pragma unroll
-    for (int it = 0; it < NE; it++)
-        if (lane + 64 * it < nE) s_inc[lane + 64 * it] = gi[it];
+        for (int it = 0; it < NE; it++) {
+            const int le = lane + 64 * it;
+            if (le < nE) {
+                const int base = 2 * K * fdiv(le, K, lg.invK);
+                const uint32_t w = L.gi[it];
+                s_slot[base + (int)(w & 0xffffu)] = (uint16_t)(2 * le - base);
+                s_slot[base + (int)(w >> 16)] = (uint16_t)(2 * le + 1 - base);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int it = 0; it < NE; it++)
+            if (lane + 64 * it < nE) s_inc[lane + 64 * it] = L.gi[it];
+    }
+    float x = L.x;
     if (acts) {
-        x = (kp.action_mode == 1) ? ((a != 0.f) ? x + stp : x - stp) : x + a;
-        if (lo > x) x = lo;     // Python max(x, originx*minl)
-        if (hi < x) x = hi;     // Python min(x, originx*maxl)
+        x = (kp.action_mode == 1) ? ((L.a != 0.f) ? x + L.stp : x - L.stp) : x + L.a;
+        if (L.lo > x) x = L.lo;     // Python max(x, originx*minl)
+        if (L.hi < x) x = L.hi;     // Python min(x, originx*maxl)
         b.muscle_x[ul] = x;
     }
     if (is_mus) s_x[lane] = x;
+    const double ym = 1.0 / (double)mf;   // IEEE 1/m of this lane's mass: every /m below is exact from it
     wave_sync();
     STAMP(1);
 
@@ -1259,17 +1362,39 @@ __device__ __forceinline__ void lean_tile(const wg_batch &b, const KParams &kp, 
     for (int it = 0; it < NE; it++) {
         const int le = lane + 64 * it;
         if (64 * it >= nE) break;                          // wave-uniform
-        const EdgeRec &e = er[it];
+        const EdgeRec &e = L.er[it];
         const int ewl = fdiv(le, K, lg.invK), ew = le - ewl * K;
         // endpoint state from the mass lanes: every lane takes part (inactive sources read as 0)
         const int bi = (ewl * M + edge_i(e.ij)) << 2, bj = (ewl * M + edge_j(e.ij)) << 2;
-        const float pix = lane_gather(p3[0], bi), piy = lane_gather(p3[1], bi), piz = lane_gather(p3[2], bi);
-        const float pjx = lane_gather(p3[0], bj), pjy = lane_gather(p3[1], bj), pjz = lane_gather(p3[2], bj);
-        const float vix = lane_gather(v3[0], bi), viy = lane_gather(v3[1], bi), viz = lane_gather(v3[2], bi);
-        const float vjx = lane_gather(v3[0], bj), vjy = lane_gather(v3[1], bj), vjz = lane_gather(v3[2], bj);
-        if (le < nE)
-            spring_edge_regs(e, le, (ew < A) ? s_x[ewl * A + ew] : e.rest, pix, piy, piz, pjx, pjy, pjz, vix, viy,
-                             viz, vjx, vjy, vjz, s_t, s_df, 0);   // lean path: spring_mode 0 only
+        const float pix = lane_gather(L.p3[0], bi), piy = lane_gather(L.p3[1], bi), piz = lane_gather(L.p3[2], bi);
+        const float pjx = lane_gather(L.p3[0], bj), pjy = lane_gather(L.p3[1], bj), pjz = lane_gather(L.p3[2], bj);
+        const float vix = lane_gather(L.v3[0], bi), viy = lane_gather(L.v3[1], bi), viz = lane_gather(L.v3[2], bi);
+        const float vjx = lane_gather(L.v3[0], bj), vjy = lane_gather(L.v3[1], bj), vjz = lane_gather(L.v3[2], bj);
+        const float xr = (le < nE && ew < A) ? s_x[ewl * A + ew] : e.rest;
+        if (QUO) {
+            const float mi = lane_gather(mf, bi), mj = lane_gather(mf, bj);
+            const double ymi = lane_gather_d(ym, bi), ymj = lane_gather_d(ym, bj);
+            if (le < nE) {
+                double t0, t1, t2;
+                float g0, g1, g2;
+                spring_terms(e, xr, pix, piy, piz, pjx, pjy, pjz, vix, viy, viz, vjx, vjy, vjz, t0, t1, t2, g0, g1,
+                             g2, 0);
+                const int base = 2 * K * ewl;
+                const uint32_t ss = *reinterpret_cast<const uint32_t *>(s_slot + base + 2 * ew);
+                // end i: a += t/m_i, a += -df/m_i; end j: a += -t/m_j, a += df/m_j
+                end_terms(t0, t1, t2, -g0, -g1, -g2, mi, ymi, s_t, s_df, base + (int)(ss & 0xffffu), lg.n2);
+                end_terms(-t0, -t1, -t2, g0, g1, g2, mj, ymj, s_t, s_df, base + (int)(ss >> 16), lg.n2);
+            }
+        } else if (le < nE) {
+            if (WG_ABLATE & 1) {   // profiling builds only: no spring arithmetic
+                s_t[3 * le] = xr + pix + pjx + vix + vjx; s_t[3 * le + 1] = piy + pjy + viy + vjy;
+                s_t[3 * le + 2] = piz + pjz + viz + vjz;
+                s_df[3 * le] = e.k; s_df[3 * le + 1] = e.c; s_df[3 * le + 2] = 0.f;
+            } else {
+                spring_edge_regs(e, le, xr, pix, piy, piz, pjx, pjy, pjz, vix, viy, viz, vjx, vjy, vjz, s_t, s_df,
+                                 0);   // lean path: spring_mode 0 only
+            }
+        }
     }
     wave_sync();
     STAMP(2);
@@ -1279,9 +1404,24 @@ __device__ __forceinline__ void lean_tile(const wg_batch &b, const KParams &kp, 
     float nv = 0.f, ke = 0.f, pe = 0.f;
     bool hit = false;
     if (is_mass) {
-        const int lb = wl * K;
-        mass_step(kp, s_t, s_df, reinterpret_cast<const uint16_t *>(s_inc) + 2 * lb, lb, io0, io1, mf,
-                  p3, v3, px, py, pz, vx, vy, vz, ax, ay, az, hit, 0, pin);
+        if (QUO) {
+            // the reference's order: per incident edge (edge order), a = f32(f64(a) + t/m), then a += df/m
+            const int base = 2 * K * wl, n2 = lg.n2;
+            const int r1 = (WG_ABLATE & 2) ? min(L.io1, L.io0 + 1) : L.io1;
+            for (int r = L.io0; r < r1; r++) {
+                const int s = base + r;
+                ax = (float)((double)ax + s_t[s]);
+                ay = (float)((double)ay + s_t[n2 + s]);
+                az = (float)((double)az + s_t[2 * n2 + s]);
+                ax = ax + s_df[s]; ay = ay + s_df[n2 + s]; az = az + s_df[2 * n2 + s];
+            }
+            mass_tail(kp, mf, (float)ym, L.p3, L.v3, px, py, pz, vx, vy, vz, ax, ay, az, hit, pin);
+        } else {
+            const int lb = wl * K;
+            mass_step(kp, s_t, s_df, reinterpret_cast<const uint16_t *>(s_inc) + 2 * lb, lb, L.io0,
+                      (WG_ABLATE & 2) ? min(L.io1, L.io0 + 1) : L.io1, mf, L.p3, L.v3, px, py, pz, vx, vy, vz, ax, ay,
+                      az, hit, 0, pin);
+        }
         nv = np_norm3(vx, vy, vz);
         ke = mf * (nv * nv);   // numpy's float32 ** 2 is libm powf: may differ by 1 ulp
         pe = (float)((double)mf * kp.g) * (py - kp.ground);
@@ -1297,8 +1437,8 @@ __device__ __forceinline__ void lean_tile(const wg_batch &b, const KParams &kp, 
     const unsigned long long gmask = (M == 64) ? ~0ull : (((1ull << M) - 1ull) << gbase);
     const unsigned long long hb = __ballot(is_mass && (py - kp.ground < 0.f));   // contacts after run1 (:200)
     const unsigned long long sb = __ballot(is_mass && nv < 0.1f);
-    const float fM = (float)M;
-    const float midx = sx / fM, midy = sy / fM, midz = sz / fM;
+    // M | 64 is a power of two: x / M == x * (1/M) exactly (the same real number, rounded once)
+    const float midx = sx * lg.invM, midy = sy * lg.invM, midz = sz * lg.invM;
     STAMP(9);
     if (is_mass) {
         float *gpo = b.pos + 3 * (size_t)pl, *gvo = b.vel + 3 * (size_t)pl, *gao = b.acc + 3 * (size_t)pl;
@@ -1308,11 +1448,11 @@ __device__ __forceinline__ void lean_tile(const wg_batch &b, const KParams &kp, 
         if (b.contact) b.contact[pl] = (uint8_t)hit;
         if (q == 0) {
             const uint32_t wg = (uint32_t)(w0 + wl);
-            const int steps = wsteps + 1;
+            const int steps = L.wsteps + 1;
             b.steps[wg] = steps;
-            const float cy = ysum / fM;
+            const float cy = ysum * lg.invM;
             if (o.reward) {
-                const float vpen = (-(vsum / fM)) * 0.1f;
+                const float vpen = (-(vsum * lg.invM)) * 0.1f;
                 o.reward[wg] = (cy + vpen) + (float)(-(double)__popcll(hb & gmask) * 0.5);
             }
             if (o.done) {
@@ -1328,7 +1468,7 @@ __device__ __forceinline__ void lean_tile(const wg_batch &b, const KParams &kp, 
     STAMP(3);
 
     // ================= observation rows: Creature.getstat (gym/optimized_walker.py:129-162) =========
-    if (o.obs) {
+    if (o.obs && !(WG_ABLATE & 16)) {
         constexpr int d = IN3D ? 3 : 2, per = 3 * d;
         const int stride = o.obs_stride, nmid = kp.conmid ? 3 : 0;
         float *otile = reinterpret_cast<float *>(s_t);
@@ -1336,7 +1476,8 @@ __device__ __forceinline__ void lean_tile(const wg_batch &b, const KParams &kp, 
         if (is_mass) {
             float *row = otile + wl * stride + per * q;
             const float pm[3] = {px, py, pz}, vm[3] = {vx, vy, vz}, am[3] = {ax, ay, az};
-            const float mm[3] = {midx, midy, midz};
+            // G1 getstat (midform 2, gym/walker.py:88-96) subtracts the SUM of positions
+            const float mm[3] = {kp.midform == 2 ? sx : midx, kp.midform == 2 ? sy : midy, kp.midform == 2 ? sz : midz};
 #pragma unroll
             for (int c = 0; c < d; c++) {
                 row[c] = kp.midform ? (pm[c] - mm[c]) * kp.pk : pm[c] * kp.pk;
@@ -1346,8 +1487,8 @@ __device__ __forceinline__ void lean_tile(const wg_batch &b, const KParams &kp, 
             if (q == 0) {
                 float *wrow = otile + wl * stride;
                 if (nmid) {
-                    wrow[per * M] = kp.midform ? midx : 0.f; wrow[per * M + 1] = kp.midform ? midy : 0.f;
-                    wrow[per * M + 2] = kp.midform ? midz : 0.f;
+                    wrow[per * M] = kp.midform ? mm[0] : 0.f; wrow[per * M + 1] = kp.midform ? mm[1] : 0.f;
+                    wrow[per * M + 2] = kp.midform ? mm[2] : 0.f;
                 }
                 for (int r = per * M + nmid + A; r < stride; r++) wrow[r] = 0.f;
             }
@@ -1368,8 +1509,21 @@ __device__ __forceinline__ void lean_tile(const wg_batch &b, const KParams &kp, 
     STAMP(6);
 }
 
-template <bool IN3D, int NE, bool PERSIST>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void walker_step_lean(
+// One wave's tile: walkers [tile*wpw, tile*wpw + wpw) of the batch, LDS slice `sl`.
+template <bool IN3D, int NE, bool QUO>
+__device__ __forceinline__ void lean_tile(const wg_batch &b, const KParams &kp, const float *__restrict__ action,
+                                          int action_cols, int action_stride, const wg_outputs &o, const LeanGeo &lg,
+                                          char *sl, int tile, int lane) {
+    const LeanTile t = lean_tile_of(b, action, action_cols, lg, tile, lane);
+    LeanIn<NE> L;
+    lean_load<NE>(b, kp, action, action_stride, t, lane, L);
+    lean_compute<IN3D, NE, QUO>(b, kp, o, lg, sl, t, lane, L);
+}
+
+// QUO's slice (~12 KB per wave for the canonical walker) holds a CU to ~3 waves per SIMD, so its register
+// budget is the 3-wave one (no spills) instead of the 6-wave one of the default path.
+template <bool IN3D, int NE, bool PERSIST, bool QUO>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QUO ? 3 : 6))) void walker_step_lean(
     wg_batch b, KParams kp, const float *__restrict__ action, int action_cols, int action_stride, wg_outputs o,
     LeanGeo lg) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1377,7 +1531,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void w
     char *sl = smem + wv * lg.slice;
     int tile = blockIdx.x * lg.wpb + wv;
     if (!PERSIST) {
-        if (tile * lg.wpw < b.N) lean_tile<IN3D, NE>(b, kp, action, action_cols, action_stride, o, lg, sl, tile, lane);
+        if (tile * lg.wpw < b.N)
+            lean_tile<IN3D, NE, QUO>(b, kp, action, action_cols, action_stride, o, lg, sl, tile, lane);
         return;
     }
     // persistent grid: a wave's tiles are tile, tile + (waves in the grid), ...
@@ -1385,7 +1540,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void w
     for (; tile * lg.wpw < b.N; tile += stride) {
         int t_opaque = tile, l_opaque = lane;
         asm volatile("" : "+v"(l_opaque), "+v"(t_opaque));   // keep per-tile index math inside the loop
-        lean_tile<IN3D, NE>(b, kp, action, action_cols, action_stride, o, lg, sl, t_opaque, l_opaque);
+        lean_tile<IN3D, NE, QUO>(b, kp, action, action_cols, action_stride, o, lg, sl, t_opaque, l_opaque);
+        wave_sync();                                          // the next tile reuses the slice
+    }
+}
+
+// Persistent waves with a one-tile register prefetch: while tile t computes, the loads of tile t + (waves in
+// the grid) are already in flight in a second LeanIn, so each wave hides its own HBM latency behind its own
+// compute instead of relying on other resident waves (the extra registers cost occupancy: 3 waves / SIMD).
+template <bool IN3D, int NE, bool QUO>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void walker_step_lean_pf(
+    wg_batch b, KParams kp, const float *__restrict__ action, int action_cols, int action_stride, wg_outputs o,
+    LeanGeo lg) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    char *sl = smem + wv * lg.slice;
+    const int ntiles = (b.N + lg.wpw - 1) / lg.wpw;
+    const int stride = gridDim.x * lg.wpb;
+    int tile = blockIdx.x * lg.wpb + wv;
+    if (tile >= ntiles) return;
+    LeanIn<NE> nxt;
+    lean_load<NE>(b, kp, action, action_stride, lean_tile_of(b, action, action_cols, lg, tile, lane), lane, nxt);
+    for (; tile < ntiles; tile += stride) {
+        const LeanIn<NE> cur = nxt;
+        if (tile + stride < ntiles)
+            lean_load<NE>(b, kp, action, action_stride, lean_tile_of(b, action, action_cols, lg, tile + stride, lane),
+                          lane, nxt);
+        lean_compute<IN3D, NE, QUO>(b, kp, o, lg, sl, lean_tile_of(b, action, action_cols, lg, tile, lane), lane, cur);
         wave_sync();                                          // the next tile reuses the slice
     }
 }
@@ -1588,11 +1769,19 @@ int launch_stream(const wg_batch *b, const KParams &kp, bool in3d, const float *
 
 // ---- lean kernel selection: uniform batch, M | 64 with M >= 4, the wave's edges in <= 8 register
 // passes, its muscles in one pass, and a workgroup LDS footprint that keeps >= 2 workgroups per CU.
-// WG_LEAN=0 selects the barrier kernels instead (A/B runs).
-bool lean_enabled() {
-    static const int m = [] { const char *e = getenv("WG_LEAN"); return e && *e ? atoi(e) : 1; }();
-    return m != 0;
+// Knobs (read on every call, so one process can A/B them): WG_LEAN=0 selects the barrier kernels;
+// WG_LEAN_PERSIST 0/1/2 (one tile per wave / persistent / persistent + prefetch); WG_LEAN_QUO 0/1 (end
+// quotients in the edge phase); WG_LEAN_WAVES 1/2/4 waves per workgroup; WG_LEAN_PER_CU, WG_LEAN_BLOCKS
+// (persistent grid size: experiments and tests).
+constexpr int LEAN_PERSIST_DEFAULT = 0;
+constexpr int LEAN_QUO_DEFAULT = 0;
+
+int env_int(const char *name, int dflt) {
+    const char *e = getenv(name);
+    return (e && *e) ? atoi(e) : dflt;
 }
+
+bool lean_enabled() { return env_int("WG_LEAN", 1) != 0; }
 
 bool lean_geo(const wg_batch *b, int obs_stride, LeanGeo *out, int spring_mode = 0) {
     const int M = b->M;
@@ -1607,42 +1796,71 @@ bool lean_geo(const wg_batch *b, int obs_stride, LeanGeo *out, int spring_mode =
     g.lgM = 0;
     while ((1 << g.lgM) < M) g.lgM++;
     if ((g.wpw * b->K + 63) / 64 > 8 || g.wpw * b->A > 64) return false;
-    const int tb = align16(std::max(g.wpw * b->K * 24, g.wpw * std::max(0, obs_stride) * 4));
-    g.off_df = tb;
-    g.off_inc = g.off_df + align16(g.wpw * b->K * 12);
-    g.off_x = g.off_inc + align16(g.wpw * b->K * 4);
-    g.slice = g.off_x + align16(std::max(1, g.wpw * b->A) * 4);
-    if (4 * g.slice > 80 * 1024) return false;
+    const int wpb = env_int("WG_LEAN_WAVES", 4);
+    g.wpb = (wpb == 1 || wpb == 2) ? wpb : 4;
+    g.persist = std::max(0, std::min(2, env_int("WG_LEAN_PERSIST", LEAN_PERSIST_DEFAULT)));
+    g.n2 = 2 * g.wpw * b->K;
+    const int obs_b = g.wpw * std::max(0, obs_stride) * 4;
+    for (int quo = (g.persist != 1 && env_int("WG_LEAN_QUO", LEAN_QUO_DEFAULT)) ? 1 : 0; quo >= 0; quo--) {
+        g.quo = quo;
+        if (quo) {   // q (f64 x3 planes) | df/m (f32 x3 planes) | slot per (edge, end) | x
+            g.off_df = align16(std::max(g.n2 * 24, obs_b));
+            g.off_inc = g.off_df + align16(g.n2 * 12);
+            g.off_x = g.off_inc + align16(g.n2 * 2);
+        } else {     // t (f64 x3 per edge) | df (f32 x3) | incidence words | x
+            g.off_df = align16(std::max(g.wpw * b->K * 24, obs_b));
+            g.off_inc = g.off_df + align16(g.wpw * b->K * 12);
+            g.off_x = g.off_inc + align16(g.wpw * b->K * 4);
+        }
+        g.slice = g.off_x + align16(std::max(1, g.wpw * b->A) * 4);
+        if (4 * g.slice <= 80 * 1024) break;
+        if (!quo) return false;
+    }
     g.invK = 1.f / (float)b->K;
     g.invA = 1.f / (float)std::max(1, b->A);
-    static const int wpb = [] { const char *e = getenv("WG_LEAN_WAVES"); return e && *e ? atoi(e) : 4; }();  // experiments
-    g.wpb = (wpb == 1 || wpb == 2) ? wpb : 4;
-    static const int persist = [] { const char *e = getenv("WG_LEAN_PERSIST"); return e && *e ? atoi(e) : 0; }();
-    g.persist = persist;
+    g.invM = 1.f / (float)M;
     *out = g;
     return true;
 }
 
-int launch_lean(const wg_batch *b, const KParams &kp, bool in3d, const float *a, int cols, int astride,
-                const wg_outputs &o, const LeanGeo &g, hipStream_t st) {
+// grid of a lean launch: one tile per wave, or the resident capacity for the persistent variants
+int lean_blocks(const wg_batch *b, const LeanGeo &g) {
     int blocks = (b->N + g.wpb * g.wpw - 1) / (g.wpb * g.wpw);
-    const int ne = (g.wpw * b->K + 63) / 64;
-    const int lds = g.wpb * g.slice;
     if (g.persist) {
         int cus = 256, dev = 0;
         if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             cus = 256;
-        const int per_cu = std::max(1, std::min((160 * 1024 - 4096) / lds, 24 / g.wpb));   // LDS share, 6 waves/SIMD
+        const int waves_cu = g.persist == 2 ? 12 : 24;   // VGPR-limited waves per CU: 3 / 6 per SIMD
+        int per_cu = std::max(1, std::min((160 * 1024 - 4096) / (g.wpb * g.slice), waves_cu / g.wpb));
+        per_cu = std::max(1, env_int("WG_LEAN_PER_CU", per_cu));
         blocks = std::min(blocks, per_cu * cus);
+        blocks = std::min(blocks, std::max(1, env_int("WG_LEAN_BLOCKS", blocks)));   // tests: many tiles per wave
     }
+    return blocks;
+}
+
+int launch_lean(const wg_batch *b, const KParams &kp, bool in3d, const float *a, int cols, int astride,
+                const wg_outputs &o, const LeanGeo &g, hipStream_t st) {
+    const int blocks = lean_blocks(b, g);
+    const int ne = (g.wpw * b->K + 63) / 64;
+    const int lds = g.wpb * g.slice;
 #define WG_LAUNCH_LEAN(D3, NE_)                                                                                  \
     do {                                                                                                         \
-        if (g.persist)                                                                                           \
-            hipLaunchKernelGGL((walker_step_lean<D3, NE_, true>), dim3(blocks), dim3(64 * g.wpb), lds, st, *b, kp, a, \
-                               cols, astride, o, g);                                                             \
+        if (g.persist == 2 && g.quo)                                                                             \
+            hipLaunchKernelGGL((walker_step_lean_pf<D3, NE_, true>), dim3(blocks), dim3(64 * g.wpb), lds, st, *b, \
+                               kp, a, cols, astride, o, g);                                                      \
+        else if (g.persist == 2)                                                                                 \
+            hipLaunchKernelGGL((walker_step_lean_pf<D3, NE_, false>), dim3(blocks), dim3(64 * g.wpb), lds, st, *b, \
+                               kp, a, cols, astride, o, g);                                                      \
+        else if (g.persist)                                                                                      \
+            hipLaunchKernelGGL((walker_step_lean<D3, NE_, true, false>), dim3(blocks), dim3(64 * g.wpb), lds, st,  \
+                               *b, kp, a, cols, astride, o, g);                                                  \
+        else if (g.quo)                                                                                          \
+            hipLaunchKernelGGL((walker_step_lean<D3, NE_, false, true>), dim3(blocks), dim3(64 * g.wpb), lds, st,  \
+                               *b, kp, a, cols, astride, o, g);                                                  \
         else                                                                                                     \
-            hipLaunchKernelGGL((walker_step_lean<D3, NE_, false>), dim3(blocks), dim3(64 * g.wpb), lds, st, *b, kp,   \
-                               a, cols, astride, o, g);                                                          \
+            hipLaunchKernelGGL((walker_step_lean<D3, NE_, false, false>), dim3(blocks), dim3(64 * g.wpb), lds, st, \
+                               *b, kp, a, cols, astride, o, g);                                                  \
     } while (0)
 #define WG_LEAN_NE(D3)                                                         \
     do {                                                                       \
@@ -1786,7 +2004,7 @@ int wg_launch_geometry(const wg_batch *b, wg_launch_info *info) {
     if (lean_geo(b, 0, &lg)) {   // the step kernel of uniform M | 64 batches (the obs tile may widen the slice)
         info->threads = 64 * lg.wpb;
         info->walkers_per_block = lg.wpb * lg.wpw;
-        info->blocks = (b->N + lg.wpb * lg.wpw - 1) / (lg.wpb * lg.wpw);
+        info->blocks = lean_blocks(b, lg);
         info->lds_bytes = lg.wpb * lg.slice;
         return 0;
     }

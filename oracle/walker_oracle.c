@@ -226,8 +226,11 @@ static void walker_observe(const orc_batch *b, const orc_params *p, int w, const
         float mid[3] = {0.f, 0.f, 0.f};
         if (p->midform) {
             for (int q = 0; q < M; q++) { mid[0] += pos[3 * q]; mid[1] += pos[3 * q + 1]; mid[2] += pos[3 * q + 2]; }
-            const float fm = (float)M;
-            mid[0] /= fm; mid[1] /= fm; mid[2] /= fm;
+            /* midform 2 = G1 Creature.getstat (gym/walker.py:88-96): the mean is never taken */
+            if (p->midform != 2) {
+                const float fm = (float)M;
+                mid[0] /= fm; mid[1] /= fm; mid[2] /= fm;
+            }
         }
         const float pk = (float)p->pk, vk = (float)p->vk, ak = (float)p->ak, mk = (float)p->mk;
         int n = 0;

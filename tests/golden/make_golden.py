@@ -74,6 +74,47 @@ def load_reference(ref: str):
     return E, OW, OE
 
 
+def load_g1_walker(ref: str, E):
+    """gym/walker.py (G1) with the two names it uses but the reference no longer provides: ``Phy(m, v, p)``
+    (undefined) and a DingPoint that is a real pinned point (gym/engine.py:569's never
+    registers and has no ``pos``).  Both create reference engine objects; ``.p`` is the G0 attribute name
+    gym/walker.py:5 reads, aliased to ``pos``."""
+    spec = importlib.util.spec_from_file_location("walker_g1", os.path.join(ref, "gym", "walker.py"))
+    G1 = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(G1)
+
+    def Phy(m, v, p):
+        pt = E.Point(m, p, v)
+        pt.p = pt.pos
+        return pt
+
+    def Ding(m, v, p):
+        pt = sys.modules["optimized_engine"].DingPoint(m, p, v)
+        pt.p = pt.pos
+        E.Point.points.append(pt)   # the env integrates it with the base Point.run1
+        return pt
+
+    G1.Phy, G1.DingPoint = Phy, Ding
+    return G1
+
+
+def load_g3(ref: str):
+    """gym/optimized_walker/{core,env,walker}.py as a package without running its __init__ (renderer/demo
+    imports; pygame is stubbed).  Returns (core, env, walker)."""
+    d = os.path.join(ref, "gym", "optimized_walker")
+    pkg = types.ModuleType("g3pkg")
+    pkg.__path__ = [d]
+    sys.modules["g3pkg"] = pkg
+    mods = []
+    for name in ("core", "renderer", "env", "walker"):
+        spec = importlib.util.spec_from_file_location("g3pkg." + name, os.path.join(d, name + ".py"))
+        mod = importlib.util.module_from_spec(spec)
+        sys.modules["g3pkg." + name] = mod
+        spec.loader.exec_module(mod)
+        mods.append(mod)
+    return mods[0], mods[2], mods[3]
+
+
 # --------------------------------------------------------------------------- scenario plumbing
 class Spec:
     """A batch in the flat CSR layout used by the oracle and the GPU path."""
@@ -113,12 +154,14 @@ class Spec:
 
 def spec_from_creatures(creatures, point_index):
     """Pack reference Creature objects (with engine Points) into a Spec (topology + state)."""
-    m, pos, vel, acc, mass_off = [], [], [], [], [0]
+    m, pos, vel, acc, mass_off, pinned = [], [], [], [], [0], []
     ei, ej, rest, k, c, flags, edge_off, nmus, minl, maxl, stride = [], [], [], [], [], [], [0], [], [], [], []
+    ding = getattr(sys.modules.get("optimized_engine"), "DingPoint", ())
     for cr in creatures:
         base = len(m)
         for p in cr.phys:
             m.append(float(p.m)); pos.append(p.pos); vel.append(p.v); acc.append(p.old_a)
+            pinned.append(1 if ding and isinstance(p, ding) else 0)
         mass_off.append(len(m))
         local = {id(p): q for q, p in enumerate(cr.phys)}
         for e in list(cr.muscles) + list(cr.skeletons):
@@ -129,7 +172,8 @@ def spec_from_creatures(creatures, point_index):
         nmus.append(len(cr.muscles))
         edge_off.append(len(ei))
         del base
-    return Spec(m, pos, vel, mass_off, ei, ej, rest, k, c, flags, edge_off, nmus, minl, maxl, stride, acc)
+    return Spec(m, pos, vel, mass_off, ei, ej, rest, k, c, flags, edge_off, nmus, minl, maxl, stride, acc,
+                pinned=pinned)
 
 
 PARAM_KEYS = ("g", "dampk", "ground", "groundk", "grounddamp", "friction", "dt", "in3d", "max_steps",
@@ -142,8 +186,8 @@ DEFAULT_PARAMS = dict(g=100.0, dampk=0.0, ground=0.0, groundk=1000.0, grounddamp
 class RefRun:
     """Drive the reference objects for one scenario and record every step."""
 
-    def __init__(self, E, OW, OE, creatures, params, action_mode="cont"):
-        self.E, self.OW, self.OE = E, OW, OE
+    def __init__(self, E, OW, OE, creatures, params, action_mode="cont", G1=None):
+        self.E, self.OW, self.OE, self.G1 = E, OW, OE, G1
         self.cr = creatures
         self.p = dict(DEFAULT_PARAMS); self.p.update(params)
         self.action_mode = action_mode
@@ -208,8 +252,12 @@ class RefRun:
         P = self.p
         out = []
         for s in self.shims:
-            obs = np.array(self.OW.Creature.getstat(s.creature, bool(P["in3d"]), P["pk"], P["vk"], P["ak"],
-                                                    P["mk"], bool(P["midform"]), bool(P["conmid"])))
+            if P["midform"] == 2:   # G1 Creature.getstat (gym/walker.py:83-101: mid is the SUM of positions)
+                obs = np.array(self.G1.Creature.getstat(s.creature, bool(P["in3d"]), P["pk"], P["vk"], P["ak"],
+                                                        P["mk"], True, bool(P["conmid"])))
+            else:
+                obs = np.array(self.OW.Creature.getstat(s.creature, bool(P["in3d"]), P["pk"], P["vk"], P["ak"],
+                                                        P["mk"], bool(P["midform"]), bool(P["conmid"])))
             o32 = obs.astype(f32)
             assert np.array_equal(o32.astype(np.float64), obs, equal_nan=True), "obs not f32-exact"
             out.append(o32)
@@ -495,6 +543,64 @@ def main():
     acts = rng2.uniform(-1, 1, (60, 2, 2)).astype(f32)
     run = RefRun(E, OW, OE, crs, dict(in3d=0, integrator=2))
     save("run2_balance", run, spec, 60, acts)
+
+    # M. G1 builders (gym/walker.py:138-353) run from the reference module itself (load_g1_walker), one of
+    #    each in a ragged batch, observed with G1 getstat (midform 2: the position SUM), 2D, 40 steps.
+    fresh()
+    G1 = load_g1_walker(args.ref, E)
+    g1_names = ["leg2", "box", "box2", "balance", "balance2", "balance3", "intrian", "humanb", "insect", "box4",
+                "leg", "hat"]
+    crs = [getattr(G1, n)() for n in g1_names]
+    for cr in crs:
+        for e in list(cr.muscles) + list(cr.skeletons):
+            e._string = 0
+        for p in cr.phys:   # the batch stores masses as float32: balance2/3's 0.1 -> f32(0.1)
+            p.m = float(np.float32(p.m))
+    spec = spec_from_creatures(crs, None)
+    acts = rng2.uniform(-1, 1, (40, spec.N, int(spec.n_muscles.max()))).astype(f32)
+    run = RefRun(E, OW, OE, crs, dict(in3d=0, midform=2, conmid=1), G1=G1)
+    save("g1_builders", run, spec, 40, acts, extra={"g1_names": np.array(g1_names)})
+
+    # N. G3 builders (gym/optimized_walker/walker.py:377-639): their points and springs as the reference's
+    #    own env methods record them (topology only; G3 physics is out of scope).  tests/golden/topology/.
+    core, g3env, g3w = load_g3(args.ref)
+
+    class _Scene:
+        def add_point(self, *a, **k):
+            pass
+
+        add_spring = add_point
+
+    class EnvRecorder:   # the state env.Environment.add_point / add_ding_point / add_spring write
+        def __init__(self):
+            self.points, self.ding_points, self.springs, self.scene = [], [], [], _Scene()
+
+    for meth in ("add_point", "add_ding_point", "add_spring"):
+        setattr(EnvRecorder, meth, getattr(g3env.Environment, meth))
+    topo = {}
+    for n, kw in (("leg2", {}), ("box", {}), ("balance1", {}), ("balance2", {}), ("balance3", {}),
+                  ("humanb", {}), ("insect", {}), ("insect8", {"legs": 8})):
+        core.Point.points = []
+        env = EnvRecorder()
+        cr = getattr(g3w, n.rstrip("8") if n == "insect8" else n)(env, **kw)
+        pts = cr.skeleton.points
+        idx = {id(p): q for q, p in enumerate(pts)}
+        topo[n + "_m"] = np.array([float(p.m) for p in pts])
+        topo[n + "_pos"] = np.array([p.pos for p in pts], f32)
+        topo[n + "_ding"] = np.array([isinstance(p, core.DingPoint) for p in pts], np.uint8)
+        topo[n + "_springs"] = np.array([[idx[id(a)], idx[id(b)]] for a, b, x, k, st in env.springs], np.int32).reshape(-1, 2)
+        topo[n + "_spring_x"] = np.array([x for a, b, x, k, st in env.springs], f32)
+        topo[n + "_spring_k"] = np.array([k for a, b, x, k, st in env.springs], np.float64)
+        topo[n + "_spring_string"] = np.array([st for a, b, x, k, st in env.springs], np.uint8)
+        mus = cr.skeleton.muscles
+        topo[n + "_muscles"] = np.array([[idx[id(mu.point1)], idx[id(mu.point2)]] for mu in mus], np.int32).reshape(-1, 2)
+        topo[n + "_muscle_x"] = np.array([mu.x for mu in mus], f32)
+        topo[n + "_muscle_power"] = np.array([mu.power for mu in mus], np.float64)
+    if args.only is None or "g3_builders" in args.only:
+        os.makedirs(os.path.join(args.out, "topology"), exist_ok=True)
+        path = os.path.join(args.out, "topology", "g3_builders.npz")
+        np.savez_compressed(path, **topo)
+        written.append(("g3_builders", os.path.getsize(path)))
 
     for name, size in written:
         print(f"{name:16s} {size:9d} B")

@@ -11,6 +11,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def cases():
     from walker_gym_amd.synthetic import canonical_walkers
+    from walker_gym_amd.topologies import topology_spec
     from walker_gym_amd.walker import balance_spec
     import numpy as np
     pinned = canonical_walkers(700, seed=13)
@@ -19,7 +20,8 @@ def cases():
     return [("canonical", canonical_walkers(1003, seed=11), dict(in3d=1), 8),   # 1003: a partial last wave
             ("balance", balance_spec(997), dict(in3d=0), 2),
             ("canonical2d", canonical_walkers(640, seed=12), dict(in3d=0, dampk=0.2, midform=0), 8),
-            ("pinned_run2", pinned, dict(in3d=1, integrator=2), 8)]
+            ("pinned_run2", pinned, dict(in3d=1, integrator=2), 8),
+            ("g1_box2", topology_spec("box2", 997, 1), dict(in3d=0, midform=2, conmid=1), 4)]
 
 
 def run(out_path):

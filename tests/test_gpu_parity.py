@@ -143,6 +143,21 @@ def test_ragged_2000_vs_oracle():
     _oracle_compare(spec, dict(in3d=1, dampk=0.3), 20, acts)
 
 
+def test_imported_topologies_vs_oracle():
+    """G1 builders (M=4 creatures take the lean kernel, observed with G1 getstat,
+    midform 2) and a ragged batch of every G3 builder (pinned m=0 pivots included)."""
+    from walker_gym_amd.topologies import G3_BUILDERS, mixed_spec, topology_spec
+    rng = np.random.default_rng(9)
+    cases = ((topology_spec("box2", 997, 1), dict(in3d=0, midform=2, conmid=1)),
+             (topology_spec("insect", 500, 1), dict(in3d=0, midform=2)),
+             (mixed_spec([(n, 40) for n in G3_BUILDERS], 3), dict(in3d=1, ground=-30.0)))
+    for spec, params in cases:
+        N = len(spec["mass_off"]) - 1
+        A = max(1, int(np.max(spec["n_muscles"])))
+        acts = rng.uniform(-1, 1, (20, N, A)).astype(np.float32)
+        _oracle_compare(spec, params, 20, acts)
+
+
 def test_full_size_sampled_vs_oracle():
     """BASELINE config 3 size (65,536 canonical walkers): walkers are independent, so the oracle
     checks a sample of them (first, last and random walkers) after 10 full-batch GPU steps."""

@@ -39,7 +39,7 @@ class EnvParams:
     vk: float = 1.0
     ak: float = 1.0
     mk: float = 1.0
-    midform: bool = True
+    midform: int = 1              # 1: minus the mean (G2 getstat); 2: minus the SUM (G1 getstat); 0: raw
     conmid: bool = False
     spring_mode: int = 0          # 0: engine.py resilience + damping; 1: G2 optimized_walker as written
     action_mode: int = 0          # 0: Muscle.act; 1: Muscle.actdisp

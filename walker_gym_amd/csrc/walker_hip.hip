@@ -711,6 +711,7 @@ __global__ __launch_bounds__(MAXT) void walker_step_kernel(
 
     // ================= per-walker reductions + outputs (gym/optimized_env.py:189-248) =================
     float midx = 0.f, midy = 0.f, midz = 0.f;
+    float sumx = 0.f, sumy = 0.f, sumz = 0.f;   // walker position sums (G1 getstat, midform 2)
     const bool is_mass = tid < nP;
     const int my_q = tid - my_lm;
     if (SHFL) {
@@ -729,6 +730,7 @@ __global__ __launch_bounds__(MAXT) void walker_step_kernel(
         const bool all_stopped = (sb & gmask) == gmask;
         const float fM = (float)M;
         midx = sx / fM; midy = sy / fM; midz = sz / fM;
+        sumx = sx; sumy = sy; sumz = sz;
         if (is_mass && my_q == 0) {
             const size_t wg = (size_t)(w0 + my_wl);
             int steps = wsteps;
@@ -832,7 +834,9 @@ __global__ __launch_bounds__(MAXT) void walker_step_kernel(
             if (is_mass) {
                 float *row = tile + (size_t)my_wl * stride + per * my_q;
                 const float pm[3] = {px, py, pz}, vm[3] = {vx, vy, vz}, am[3] = {ax, ay, az};
-                const float mm[3] = {midx, midy, midz};
+                // G1 getstat (midform 2, gym/walker.py:88-96) subtracts the SUM of positions
+                const float mm[3] = {kp.midform == 2 ? sumx : midx, kp.midform == 2 ? sumy : midy,
+                                     kp.midform == 2 ? sumz : midz};
 #pragma unroll
                 for (int c = 0; c < d; c++) {
                     row[c] = kp.midform ? (pm[c] - mm[c]) * kp.pk : pm[c] * kp.pk;
@@ -841,7 +845,7 @@ __global__ __launch_bounds__(MAXT) void walker_step_kernel(
                 }
                 if (my_q == 0 && nmid) {
                     float *wrow = tile + (size_t)my_wl * stride + per * b.M;
-                    wrow[0] = kp.midform ? midx : 0.f; wrow[1] = kp.midform ? midy : 0.f; wrow[2] = kp.midform ? midz : 0.f;
+                    wrow[0] = kp.midform ? mm[0] : 0.f; wrow[1] = kp.midform ? mm[1] : 0.f; wrow[2] = kp.midform ? mm[2] : 0.f;
                 }
                 if (my_q == 0)
                     for (int r = per * b.M + nmid + b.A; r < stride; r++) tile[(size_t)my_wl * stride + r] = 0.f;
@@ -859,7 +863,8 @@ __global__ __launch_bounds__(MAXT) void walker_step_kernel(
 #pragma unroll
                 for (int c = 0; c < d; c++) {
                     const float pv = s.pos[3 * lp + c];
-                    row[c] = kp.midform ? (pv - s.red[8 * wl + c] / fM) * kp.pk : pv * kp.pk;
+                    const float mid = kp.midform == 2 ? s.red[8 * wl + c] : s.red[8 * wl + c] / fM;   // G1: the sum
+                    row[c] = kp.midform ? (pv - mid) * kp.pk : pv * kp.pk;
                     row[d + c] = s.vel[3 * lp + c] * kp.vk;
                     row[2 * d + c] = s.acc[3 * lp + c] * kp.ak;
                 }
@@ -871,7 +876,8 @@ __global__ __launch_bounds__(MAXT) void walker_step_kernel(
                 const int A = RAGGED ? s.uoff[wl + 1] - s.uoff[wl] : b.A;
                 float *row = (RAGGED ? ob : tile) + (size_t)wl * stride;
                 if (nmid)
-                    for (int c = 0; c < 3; c++) row[per * M + c] = kp.midform ? s.red[8 * wl + c] / (float)M : 0.f;
+                    for (int c = 0; c < 3; c++)
+                        row[per * M + c] = kp.midform == 2 ? s.red[8 * wl + c] : kp.midform ? s.red[8 * wl + c] / (float)M : 0.f;
                 for (int r = per * M + nmid + A; r < stride; r++) row[r] = 0.f;
             }
         }
@@ -1046,7 +1052,7 @@ __global__ __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(4, 8))) vo
             if (is_mass) {
                 float *row = tile_obs + (size_t)my_wl * stride + per * my_q;
                 const float pm3[3] = {px, py, pz}, vm3[3] = {vx, vy, vz}, am3[3] = {ax, ay, az};
-                const float mm3[3] = {midx, midy, midz};
+                const float mm3[3] = {kp.midform == 2 ? sx : midx, kp.midform == 2 ? sy : midy, kp.midform == 2 ? sz : midz};
                 _Pragma("unroll") for (int c = 0; c < d; c++) {
                     row[c] = kp.midform ? (pm3[c] - mm3[c]) * kp.pk : pm3[c] * kp.pk;
                     row[d + c] = vm3[c] * kp.vk;
@@ -1055,8 +1061,8 @@ __global__ __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(4, 8))) vo
                 if (my_q == 0) {
                     float *wrow = tile_obs + (size_t)my_wl * stride;
                     if (nmid) {
-                        wrow[per * M] = kp.midform ? midx : 0.f; wrow[per * M + 1] = kp.midform ? midy : 0.f;
-                        wrow[per * M + 2] = kp.midform ? midz : 0.f;
+                        wrow[per * M] = kp.midform ? mm3[0] : 0.f; wrow[per * M + 1] = kp.midform ? mm3[1] : 0.f;
+                        wrow[per * M + 2] = kp.midform ? mm3[2] : 0.f;
                     }
                     for (int r = per * M + nmid + A; r < stride; r++) wrow[r] = 0.f;
                 }

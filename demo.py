@@ -31,8 +31,7 @@ def main():
         cr = build_creature(a.g1, generation=1)
         env = Environment([cr], in3d=False)
         for t in range(a.steps):
-            cr.act(rng.uniform(-1, 1, len(cr.muscles)))   # host-side muscle state before packing is ignored
-            env.step(0.01)
+            env.step(0.01)                              # gym/env.py:48-50 (no actions in the G1 loop)
         print(f"{a.g1}: {a.steps} steps, centroid {np.mean([p.pos for p in cr.phys], axis=0)}")
         return
     from walker_gym_amd.optimized_env import make_env

@@ -22,6 +22,7 @@ VARIANTS = {
     "quo_w1": {"WG_LEAN_QUO": "1", "WG_LEAN_WAVES": "1"},
     "quo_pf": {"WG_LEAN_QUO": "1", "WG_LEAN_PERSIST": "2"},
     "lean_w2": {"WG_LEAN_WAVES": "2"},
+    "lean_w1": {"WG_LEAN_WAVES": "1"},
 }
 KEYS = ("WG_LEAN_PERSIST", "WG_LEAN_QUO", "WG_LEAN_WAVES", "WG_LEAN_PER_CU", "WG_LEAN_BLOCKS")
 

@@ -357,16 +357,18 @@ __device__ __forceinline__ void mass_tail(const KParams &kp, float mf, float ymf
         ax = ax + fdiv_mk((-vx) * ff, mf, ymf); ay = ay + zm; az = az + fdiv_mk((-vz) * ff, mf, ymf);
     }
     if (pinned) { ax = 0.f; ay = 0.f; az = 0.f; }   // DingPoint.forced is a no-op: a stays zeros()
-    if (kp.integrator == 2) {
-        // Point.run2 (gym/engine.py:184-187): pos += v*t + 0.5*a*t**2 (numpy: (v*t) + ((0.5*a)*f32(t**2))), v += a*t
-        px = px + (vx * kp.dt + (0.5f * ax) * kp.dt2);
-        py = py + (vy * kp.dt + (0.5f * ay) * kp.dt2);
-        pz = pz + (vz * kp.dt + (0.5f * az) * kp.dt2);
-        vx = vx + ax * kp.dt; vy = vy + ay * kp.dt; vz = vz + az * kp.dt;
-    } else {
-        vx = vx + ax * kp.dt; vy = vy + ay * kp.dt; vz = vz + az * kp.dt;   // Point.run1
-        px = px + vx * kp.dt; py = py + vy * kp.dt; pz = pz + vz * kp.dt;
-    }
+    // v += a*t in both integrators; the position update differs.  Both forms are computed and one selected:
+    // an if/else over px..vz references made hipcc keep them in a dynamically indexed stack array (scratch).
+    const float nvx = vx + ax * kp.dt, nvy = vy + ay * kp.dt, nvz = vz + az * kp.dt;
+    // Point.run1 (gym/engine.py:174-178): pos += v_new*t
+    const float p1x = px + nvx * kp.dt, p1y = py + nvy * kp.dt, p1z = pz + nvz * kp.dt;
+    // Point.run2 (gym/engine.py:184-187): pos += v*t + 0.5*a*t**2 (numpy: (v*t) + ((0.5*a)*f32(t**2)))
+    const float p2x = px + (vx * kp.dt + (0.5f * ax) * kp.dt2);
+    const float p2y = py + (vy * kp.dt + (0.5f * ay) * kp.dt2);
+    const float p2z = pz + (vz * kp.dt + (0.5f * az) * kp.dt2);
+    const bool run2 = kp.integrator == 2;
+    px = run2 ? p2x : p1x; py = run2 ? p2y : p1y; pz = run2 ? p2z : p1z;
+    vx = nvx; vy = nvy; vz = nvz;
 }
 
 // Mass `lp`: the ordered force accumulation over its incidence list (edge order, spring then damping
@@ -1366,9 +1368,11 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
     // ================= springs: gym/engine.py:78-102 + gym/optimized_walker.py:92-106 =================
 #pragma unroll
     for (int it = 0; it < NE; it++) {
+        // a by-value record and no early loop exit: both keep er[] in registers (a reference under a `break`
+        // made hipcc park the rest lengths in scratch right after their loads, serialising them)
+        if (64 * it >= nE) continue;                       // wave-uniform
         const int le = lane + 64 * it;
-        if (64 * it >= nE) break;                          // wave-uniform
-        const EdgeRec &e = L.er[it];
+        const EdgeRec e = L.er[it];
         const int ewl = fdiv(le, K, lg.invK), ew = le - ewl * K;
         // endpoint state from the mass lanes: every lane takes part (inactive sources read as 0)
         const int bi = (ewl * M + edge_i(e.ij)) << 2, bj = (ewl * M + edge_j(e.ij)) << 2;

@@ -84,7 +84,7 @@ def load_traffic(workload: str, walkers: int):
     """HBM bytes per launch from a committed rocprofv3 PMC run (profiles/*pmc*.json), if present."""
     import glob
     best = None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), key=os.path.getmtime):   # newest last
         try:
             d = json.load(open(f))
         except Exception:

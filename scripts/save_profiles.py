@@ -34,7 +34,7 @@ summ = os.path.join(g, f"{pmc_tag}_summary.json")
 if os.path.exists(summ):
     c = json.load(open(summ))
     hbm = (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
-    json.dump({"workload": "canonical", "walkers": 65536, "kernel": "walker_step_lean<true,3,false> (default uniform path)",
+    json.dump({"workload": "canonical", "walkers": 65536, "kernel": "walker_step_lean<true,3,false,false> (default uniform path)",
                "source": "rocprofv3 --pmc, 6 separate passes over scripts/prof_run.py (65536 canonical walkers, "
                          "30 steps), per-dispatch averages (scripts/gpu_pmc.sh, scripts/pmc_summary.py)",
                "hbm_bytes_per_launch": round(hbm),

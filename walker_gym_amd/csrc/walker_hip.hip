@@ -636,7 +636,7 @@ __global__ __launch_bounds__(MAXT) void walker_step_kernel(
 #pragma unroll
             for (int it = 0; it < EPL; it++) {
                 const int le = tid + (pass * EPL + it) * T;
-                if (le >= nE) break;
+                if (le >= nE) continue;   // (not break: an early exit kept er[] on the stack)
                 const EdgeRec e = (pass == 0) ? er[it] : load_edge(b.edges, E0 + le);
                 if (WG_ABLATE & 1) {
                     s.t[3 * le] = e.rest; s.t[3 * le + 1] = e.k; s.t[3 * le + 2] = e.c;

@@ -24,7 +24,7 @@ class OrcParams(C.Structure):
     _fields_ = [(n, C.c_double) for n in ("g", "dampk", "ground", "groundk", "grounddamp", "friction",
                                            "dt", "pk", "vk", "ak", "mk")] + \
                [(n, C.c_int32) for n in ("in3d", "max_steps", "midform", "conmid", "spring_mode",
-                                         "action_mode", "integrator")]
+                                         "action_mode", "integrator", "pair_mode")] + [("pair_g", C.c_double)]
 
 
 class OrcBatch(C.Structure):
@@ -72,7 +72,7 @@ def _p(a, t):
 
 DEFAULT_PARAMS = dict(g=100.0, dampk=0.0, ground=0.0, groundk=1000.0, grounddamp=100.0, friction=100.0,
                       dt=0.01, in3d=1, max_steps=1000, pk=1.0, vk=1.0, ak=1.0, mk=1.0, midform=1,
-                      conmid=0, spring_mode=0, action_mode=0, integrator=1)
+                      conmid=0, spring_mode=0, action_mode=0, integrator=1, pair_mode=0, pair_g=9.8)
 
 
 class Oracle:

@@ -170,6 +170,23 @@ static void walker_step(const orc_batch *b, const orc_params *p, int w, const fl
         }
     }
 
+    /* 3b. pair_mode 1: Point.gravity (gym/engine.py:128-137) over this walker's masses.  For each pair i < j:
+     *     r = max(norm(pos_i - pos_j) as float64, Config.r); f = -g * m_i * m_j / r**2 (Python floats);
+     *     j.anti_forced(f, i) then i.anti_forced(f, j) (:69-76): force = -f * direction / distance, all
+     *     float64 (f is a numpy float64 scalar: r came from .astype(float)); forced: a += force / m
+     *     (float64, rounded to float32). */
+    if (p->pair_mode == 1) {
+        for (int i = m0; i < m1; i++)
+            for (int j = i + 1; j < m1; j++) {
+                const float *pi = pos + 3 * i, *pj = pos + 3 * j;
+                double r = (double)np_norm3(pi[0] - pj[0], pi[1] - pj[1], pi[2] - pj[2]);
+                if (CONFIG_R > r) r = CONFIG_R;
+                const double f = ((-p->pair_g) * (double)b->m[i]) * (double)b->m[j] / (r * r);
+                for (int c = 0; c < 3; c++) acc[3 * j + c] = add_f64(acc[3 * j + c], (-f) * (double)(pi[c] - pj[c]) / r, b->m[j]);
+                for (int c = 0; c < 3; c++) acc[3 * i + c] = add_f64(acc[3 * i + c], (-f) * (double)(pj[c] - pi[c]) / r, b->m[i]);
+            }
+    }
+
     /* 4. env forces per mass (gym/env.py:31-41, gym/optimized_env.py:146-172), each one Point.forced
      *    with a float32 force: gravity, linear damp, then (in contact) ground spring, ground damp,
      *    friction |deep|*friction (optimized_env.py:168-172 form). */

@@ -19,6 +19,8 @@ typedef struct orc_params {
     int32_t spring_mode;   /* 0 = engine.py resilience + G2 damping; 1 = G2 optimized_walker as written */
     int32_t action_mode;   /* 0 = Muscle.act (continuous); 1 = Muscle.actdisp (discrete) */
     int32_t integrator;    /* 0/1 = Point.run1 (gym/engine.py:168-178); 2 = Point.run2 (:180-190) */
+    int32_t pair_mode;     /* 1 = per-walker Point.gravity (gym/engine.py:128-137) after the springs */
+    double pair_g;         /* its Config.g */
 } orc_params;
 
 typedef struct orc_batch {

@@ -177,10 +177,10 @@ def spec_from_creatures(creatures, point_index):
 
 
 PARAM_KEYS = ("g", "dampk", "ground", "groundk", "grounddamp", "friction", "dt", "in3d", "max_steps",
-              "pk", "vk", "ak", "mk", "midform", "conmid", "spring_mode", "integrator")
+              "pk", "vk", "ak", "mk", "midform", "conmid", "spring_mode", "integrator", "pair_mode", "pair_g")
 DEFAULT_PARAMS = dict(g=100.0, dampk=0.0, ground=0.0, groundk=1000.0, grounddamp=100.0, friction=100.0,
                       dt=0.01, in3d=1, max_steps=1000, pk=1.0, vk=1.0, ak=1.0, mk=1.0, midform=1,
-                      conmid=0, spring_mode=0, integrator=1)
+                      conmid=0, spring_mode=0, integrator=1, pair_mode=0, pair_g=9.8)
 
 
 class RefRun:
@@ -223,6 +223,11 @@ class RefRun:
                     continue
                 e.p1.resilience(e.p2, e.x, e.k, bool(getattr(e, "_string", 0)))   # gym/engine.py:78
                 OW.Skeleton(e.p1, e.p2, x=e.x, k=0, dampk=e.dampk).run()          # damping only
+            if P["pair_mode"] == 1:                # gym/engine.py:128-137 over this walker's points only
+                saved, g0 = E.Point.points, E.Config.g
+                E.Point.points, E.Config.g = list(cr.phys), P["pair_g"]
+                E.Point.gravity()
+                E.Point.points, E.Config.g = saved, g0
             for p in cr.phys:                      # gym/optimized_env.py:146-172 with forces as f32 arrays
                 p.forced(np.array([0, -P["g"], 0], dtype=f32))
                 p.forced(np.asarray(-P["dampk"] * p.v, dtype=f32))
@@ -321,7 +326,8 @@ def pad_obs(obs_list):
 
 def params_array(p):
     # integrator is recorded only where it is not the default, so the older fixtures stay byte-stable
-    return {"param_" + k: np.array(p[k]) for k in PARAM_KEYS if k != "integrator" or p[k] != 1}
+    keep = lambda k: (k != "integrator" or p[k] != 1) and (k not in ("pair_mode", "pair_g") or p["pair_mode"] != 0)
+    return {"param_" + k: np.array(p[k]) for k in PARAM_KEYS if keep(k)}
 
 
 # --------------------------------------------------------------------------- creature builders
@@ -543,6 +549,21 @@ def main():
     acts = rng2.uniform(-1, 1, (60, 2, 2)).astype(f32)
     run = RefRun(E, OW, OE, crs, dict(in3d=0, integrator=2))
     save("run2_balance", run, spec, 60, acts)
+
+    # O. per-walker pair gravity (gym/engine.py:128-137 restricted to each walker, after the springs):
+    #    canonical walkers (3D) and Balance-v0 (2D), Config.g raised so the pair forces matter, 60 steps.
+    for name, sp, in3d, A, pg in (("pair_gravity_canonical", canonical_walkers(3, seed=31), 1, 8, 2000.0),
+                                  ("pair_gravity_balance", None, 0, 2, 5.0e4)):
+        fresh()
+        if sp is None:
+            crs = reference_builders(E, OW, "balance", 2)
+            spec = spec_from_creatures(crs, None)
+        else:
+            spec = Spec(**sp)
+            crs = creatures_from_spec(E, OW, spec)
+        acts = rng2.uniform(-1, 1, (60, spec.N, A)).astype(f32)
+        run = RefRun(E, OW, OE, crs, dict(in3d=in3d, pair_mode=1, pair_g=pg))
+        save(name, run, spec, 60, acts)
 
     # M. G1 builders (gym/walker.py:138-353) run from the reference module itself (load_g1_walker), one of
     #    each in a ragged batch, observed with G1 getstat (midform 2: the position SUM), 2D, 40 steps.

@@ -51,7 +51,7 @@ int main(void) {
   printf("wg_params %zu\\nwg_batch %zu\\nwg_outputs %zu\\nwg_edge %zu\\nwg_launch_info %zu\\n",
          sizeof(wg_params), sizeof(wg_batch), sizeof(wg_outputs), sizeof(wg_edge), sizeof(wg_launch_info));
   F(wg_batch, pos) F(wg_batch, edges) F(wg_batch, inc_off) F(wg_batch, muscle_bounds) F(wg_batch, contact)
-  F(wg_outputs, obs_step) F(wg_outputs, out_step) F(wg_params, in3d) F(wg_params, action_mode)
+  F(wg_outputs, obs_step) F(wg_outputs, out_step) F(wg_params, in3d) F(wg_params, action_mode) F(wg_params, pair_g)
   return 0;
 }
 """)
@@ -80,6 +80,15 @@ def test_errors_without_gpu(lib):
     assert lib.wg_step(C.byref(b), C.byref(p), None, 0, 0, 0, None, 1, None, 0, None) == _lib.WG_ERANGE
     with pytest.raises(ValueError):
         _lib.check(-1, "probe")
+    # pair gravity runs on the wave-per-walker-group kernel only: a ragged batch is refused before any launch
+    b = _lib.WgBatch(N=4, M=8, K=4, A=0, ragged=1)
+    for f in ("pos", "vel", "acc", "mass", "edges", "inc", "inc_off", "muscle_x", "steps", "mass_off", "edge_off",
+              "muscle_off"):
+        setattr(b, f, 16)
+    p = _lib.WgParams(pair_mode=1, pair_g=9.8)
+    plan = np.zeros(2, np.int32)
+    assert lib.wg_step(C.byref(b), C.byref(p), None, 0, 0, 0, None, 1, plan.ctypes.data_as(C.c_void_p), 1, None) == _lib.WG_EINVAL
+    assert b"pair_mode" in lib.wg_last_error()
 
 
 def test_plan_ragged_host(lib):

@@ -13,7 +13,7 @@ import threading
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libwalker_hip.so"
 LIB_PATH = os.path.join(HERE, LIB_NAME)
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 WG_EINVAL, WG_ERANGE, WG_EHIP = -1, -2, -3
 
@@ -24,7 +24,7 @@ class WgParams(C.Structure):
     _fields_ = [(n, C.c_double) for n in ("g", "dampk", "ground", "groundk", "grounddamp", "friction", "dt",
                                            "pk", "vk", "ak", "mk")] + \
                [(n, C.c_int32) for n in ("in3d", "max_steps", "midform", "conmid", "spring_mode", "action_mode",
-                                         "integrator")]
+                                         "integrator", "pair_mode")] + [("pair_g", C.c_double)]
 
 
 class WgBatch(C.Structure):

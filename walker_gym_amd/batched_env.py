@@ -44,6 +44,8 @@ class EnvParams:
     spring_mode: int = 0          # 0: engine.py resilience + damping; 1: G2 optimized_walker as written
     action_mode: int = 0          # 0: Muscle.act; 1: Muscle.actdisp
     integrator: int = 1           # 1: Point.run1 (what the envs call); 2: Point.run2 (gym/engine.py:180-190)
+    pair_mode: int = 0            # 1: per-walker Point.gravity (gym/engine.py:128-137) after the springs
+    pair_g: float = 9.8           # Config.g of that pass (gym/engine.py:12)
 
     def to_struct(self) -> _lib.WgParams:
         d = asdict(self)
@@ -52,7 +54,7 @@ class EnvParams:
         if int(d["integrator"]) not in (0, 1, 2):
             raise ValueError("integrator must be 1 ('run1') or 2 ('run2')")
         return _lib.WgParams(**{k: (int(v) if k in ("in3d", "max_steps", "midform", "conmid", "spring_mode",
-                                                    "action_mode", "integrator") else float(v))
+                                                    "action_mode", "integrator", "pair_mode") else float(v))
                                 for k, v in d.items()})
 
 

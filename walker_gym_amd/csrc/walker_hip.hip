@@ -76,6 +76,8 @@ struct KParams {
     double g;
     int max_steps, midform, conmid, spring_mode, action_mode;
     int integrator; // 2: Point.run2, otherwise Point.run1
+    int pair_mode;  // 1: per-walker Point.gravity after the springs (lean kernel)
+    double pair_g;
     int stagger;    // diagnostics (WG_STAGGER): blocks with blockIdx % 4 == k idle k*stagger*64 cycles first
 };
 
@@ -375,11 +377,9 @@ __device__ __forceinline__ void mass_tail(const KParams &kp, float mf, float ymf
 // per edge — gym/optimized_walker.py:124-127 with gym/engine.py:65-76, 101-102), then gravity, linear
 // damping and the ground penalty (gym/env.py:31-41 / gym/optimized_env.py:146-172, each one
 // Point.forced), then Point.run1 (gym/engine.py:174-178).  Returns the new state and old_a.
-__device__ __forceinline__ void mass_step(const KParams &kp, const double *st, const float *sdf,
-                                          const uint16_t *inc, int lb, int s0, int s1, float mf,
-                                          const float *p3, const float *v3, float &px, float &py, float &pz,
-                                          float &vx, float &vy, float &vz, float &ax, float &ay, float &az,
-                                          bool &hit, int spring_mode, bool pinned) {
+__device__ __forceinline__ void mass_accumulate(const double *st, const float *sdf, const uint16_t *inc, int lb,
+                                                int s0, int s1, float mf, float &ax, float &ay, float &az,
+                                                int spring_mode) {
     const double md = (double)mf;
     const double ym = 1.0 / md;      // one IEEE division per mass; every /m below is exact from it
     const float ymf = (float)ym;     // = RN32(1/m)
@@ -450,6 +450,15 @@ __device__ __forceinline__ void mass_step(const KParams &kp, const double *st, c
             }
         }
     }
+}
+
+__device__ __forceinline__ void mass_step(const KParams &kp, const double *st, const float *sdf,
+                                          const uint16_t *inc, int lb, int s0, int s1, float mf,
+                                          const float *p3, const float *v3, float &px, float &py, float &pz,
+                                          float &vx, float &vy, float &vz, float &ax, float &ay, float &az,
+                                          bool &hit, int spring_mode, bool pinned) {
+    mass_accumulate(st, sdf, inc, lb, s0, s1, mf, ax, ay, az, spring_mode);
+    const float ymf = (float)(1.0 / (double)mf);
     mass_tail(kp, mf, ymf, p3, v3, px, py, pz, vx, vy, vz, ax, ay, az, hit, pinned);
 }
 
@@ -1308,6 +1317,32 @@ __device__ __forceinline__ void end_terms(double t0, double t1, double t2, float
     sqd[slot] = c0; sqd[n2 + slot] = c1; sqd[2 * n2 + slot] = c2;
 }
 
+// pair_mode 1: Point.gravity (gym/engine.py:128-137) restricted to the walker's masses, after its springs
+// (SURVEY §8(f) 3).  Mass q meets its partners in the reference pair loop's order (i < j): ascending
+// partner index.  Per partner: r = max(norm(p_i - p_j) as float64, Config.r); f = -g*m_i*m_j/r**2 in float64
+// (i the lower index); anti_forced (:69-76): force = (-f * (p_partner - p_q)) / r, all float64 (f is a numpy
+// float64 scalar, r came from .astype(float)); forced (:65-67): a = f32(f64(a) + force/m).  Every lane runs the loop (partner state by ds_bpermute); non-mass lanes
+// discard theirs.  IEEE float64 divisions: an opt-in mode, not the headline path.
+__device__ __forceinline__ void pair_gravity(const KParams &kp, const float *p3, float mf, int lane, int M,
+                                             bool is_mass, float &ax, float &ay, float &az) {
+    const int gb = lane & ~(M - 1), q = lane & (M - 1);
+    const double md = (double)mf;
+    for (int pj = 0; pj < M; pj++) {
+        const int src = (gb + pj) << 2;
+        const float ox = lane_gather(p3[0], src), oy = lane_gather(p3[1], src), oz = lane_gather(p3[2], src);
+        const float om = lane_gather(mf, src);
+        if (!is_mass || pj == q) continue;
+        const float d0 = ox - p3[0], d1 = oy - p3[1], d2 = oz - p3[2];   // partner - self
+        double r = (double)np_norm3(d0, d1, d2);      // == norm(p_i - p_j): the squares do not see the sign
+        if (CONFIG_R > r) r = CONFIG_R;
+        const double mlo = pj < q ? (double)om : md, mhi = pj < q ? md : (double)om;
+        const double f = ((-kp.pair_g) * mlo) * mhi / (r * r);
+        ax = (float)((double)ax + ((-f) * (double)d0 / r) / md);
+        ay = (float)((double)ay + ((-f) * (double)d1 / r) / md);
+        az = (float)((double)az + ((-f) * (double)d2 / r) / md);
+    }
+}
+
 // One wave's tile after its loads.  QUO = false: the edge lanes leave the spring term t and the damping
 // force df per edge in LDS, the mass lanes divide by m while walking their incidence lists (mass_step).
 // QUO = true: the edge lanes also form both ends' quotients (end_terms, edge-parallel: 83 % lane use for the
@@ -1414,10 +1449,10 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
     float nv = 0.f, ke = 0.f, pe = 0.f;
     bool hit = false;
     if (is_mass) {
+        const int r1 = (WG_ABLATE & 2) ? min(L.io1, L.io0 + 1) : L.io1;
         if (QUO) {
             // the reference's order: per incident edge (edge order), a = f32(f64(a) + t/m), then a += df/m
             const int base = 2 * K * wl, n2 = lg.n2;
-            const int r1 = (WG_ABLATE & 2) ? min(L.io1, L.io0 + 1) : L.io1;
             for (int r = L.io0; r < r1; r++) {
                 const int s = base + r;
                 ax = (float)((double)ax + s_t[s]);
@@ -1425,13 +1460,15 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
                 az = (float)((double)az + s_t[2 * n2 + s]);
                 ax = ax + s_df[s]; ay = ay + s_df[n2 + s]; az = az + s_df[2 * n2 + s];
             }
-            mass_tail(kp, mf, (float)ym, L.p3, L.v3, px, py, pz, vx, vy, vz, ax, ay, az, hit, pin);
         } else {
             const int lb = wl * K;
-            mass_step(kp, s_t, s_df, reinterpret_cast<const uint16_t *>(s_inc) + 2 * lb, lb, L.io0,
-                      (WG_ABLATE & 2) ? min(L.io1, L.io0 + 1) : L.io1, mf, L.p3, L.v3, px, py, pz, vx, vy, vz, ax, ay,
-                      az, hit, 0, pin);
+            mass_accumulate(s_t, s_df, reinterpret_cast<const uint16_t *>(s_inc) + 2 * lb, lb, L.io0, r1, mf, ax, ay,
+                            az, 0);
         }
+    }
+    if (kp.pair_mode == 1) pair_gravity(kp, L.p3, mf, lane, M, is_mass, ax, ay, az);   // every lane (gathers)
+    if (is_mass) {
+        mass_tail(kp, mf, (float)ym, L.p3, L.v3, px, py, pz, vx, vy, vz, ax, ay, az, hit, pin);
         nv = np_norm3(vx, vy, vz);
         ke = mf * (nv * nv);   // numpy's float32 ** 2 is libm powf: may differ by 1 ulp
         pe = (float)((double)mf * kp.g) * (py - kp.ground);
@@ -1621,6 +1658,8 @@ KParams make_kparams(const wg_params &p) {
     k.max_steps = p.max_steps; k.midform = p.midform; k.conmid = p.conmid;
     k.spring_mode = p.spring_mode; k.action_mode = p.action_mode;
     k.integrator = p.integrator;
+    k.pair_mode = p.pair_mode;
+    k.pair_g = p.pair_g;
     k.dt2 = (float)(p.dt * p.dt);
     static const int stagger = [] { const char *e = getenv("WG_STAGGER"); return e ? atoi(e) : 0; }();
     k.stagger = stagger;
@@ -1915,6 +1954,9 @@ int run(const wg_batch *b, const wg_params *p, const float *action, int32_t cols
     const int blocks = b->ragged ? plan_blocks : (b->N + g.W - 1) / g.W;
     LeanGeo lg{};
     const bool use_lean = step && lean_geo(b, out.obs ? out.obs_stride : 0, &lg, p->spring_mode);
+    if (step && p->pair_mode != 0 && (p->pair_mode != 1 || !use_lean))
+        return fail(WG_EINVAL, "pair_mode %d needs pair_mode 1 on a uniform batch with M | 64 (4 <= M <= 64), "
+                               "spring_mode 0", p->pair_mode);
     for (int s = 0; s < n_steps; s++) {
         wg_outputs os = out;
         if (os.obs) os.obs += s * os.obs_step;

@@ -105,34 +105,38 @@ struct Carve {
 
 __host__ __device__ inline int align16(int b) { return (b + 15) & ~15; }
 
-// one carve for host sizing and device pointers: `base == nullptr` only sums the sizes
-__host__ __device__ inline int carve_walk(const Geo &g, char *base, Carve *c) {
-    int b = 0;
-    auto take = [&](int bytes) { char *p = base ? base + b : nullptr; b += align16(bytes); return p; };
+// one carve for host sizing and device pointers.  The walk produces byte OFFSETS only; the device
+// pointers are `smem + offset` with no null test in between, so the compiler keeps them in the LDS
+// address space (a `base ? base + b : nullptr` select made them generic: flat loads/stores and the
+// 15 pointers spilled to scratch in the ragged kernel).
+enum { CV_T, CV_POS, CV_VEL, CV_ACC, CV_M, CV_DF, CV_INC, CV_X, CV_NRM, CV_KE, CV_PE, CV_RED,
+       CV_MOFF, CV_EOFF, CV_UOFF, CV_N };
+__host__ __device__ inline int carve_walk(const Geo &g, int *off) {
+    int b = 0, k = 0;
+    auto take = [&](int bytes) { off[k++] = b; b += align16(bytes); };
     const int full = g.lite ? 0 : 1;
-    char *t = take(g.tbytes), *pos = take(g.Pcap * 12), *vel = take(g.Pcap * 12);
-    char *acc = take(full * g.Pcap * 12), *m = take(full * g.Pcap * 4);
-    char *df = take(std::max(g.Ecap * 12, g.stage * g.Pcap * 36));   // streaming kernel: also the out-stage
-    char *inc = take(g.Ecap * 4 + 16), *x = take(g.Ucap * 4);
-    char *nrm = take(full * g.Pcap * 4), *ke = take(full * g.Pcap * 4), *pe = take(full * g.Pcap * 4);
-    char *red = take(full * g.W * 32);
-    char *moff = take(full * (g.W + 1) * 4), *eoff = take(full * (g.W + 1) * 4), *uoff = take(full * (g.W + 1) * 4);
-    if (c) {
-        c->t = reinterpret_cast<double *>(t); c->pos = reinterpret_cast<float *>(pos);
-        c->vel = reinterpret_cast<float *>(vel); c->acc = reinterpret_cast<float *>(acc);
-        c->m = reinterpret_cast<float *>(m); c->df = reinterpret_cast<float *>(df);
-        c->inc = reinterpret_cast<uint32_t *>(inc); c->x = reinterpret_cast<float *>(x);
-        c->nrm = reinterpret_cast<float *>(nrm); c->ke = reinterpret_cast<float *>(ke);
-        c->pe = reinterpret_cast<float *>(pe); c->red = reinterpret_cast<float *>(red);
-        c->moff = reinterpret_cast<int *>(moff); c->eoff = reinterpret_cast<int *>(eoff);
-        c->uoff = reinterpret_cast<int *>(uoff);
-    }
+    take(g.tbytes); take(g.Pcap * 12); take(g.Pcap * 12);                  // t, pos, vel
+    take(full * g.Pcap * 12); take(full * g.Pcap * 4);                      // acc, m
+    take(std::max(g.Ecap * 12, g.stage * g.Pcap * 36));                    // df (streaming kernel: also the out-stage)
+    take(g.Ecap * 4 + 16); take(g.Ucap * 4);                                // inc, x
+    take(full * g.Pcap * 4); take(full * g.Pcap * 4); take(full * g.Pcap * 4);   // nrm, ke, pe
+    take(full * g.W * 32);                                                  // red
+    take(full * (g.W + 1) * 4); take(full * (g.W + 1) * 4); take(full * (g.W + 1) * 4);   // moff, eoff, uoff
     return b;
 }
-__host__ __device__ inline int carve_bytes(const Geo &g) { return carve_walk(g, nullptr, nullptr); }
+__host__ __device__ inline int carve_bytes(const Geo &g) { int off[CV_N]; return carve_walk(g, off); }
 __device__ inline Carve carve(char *s, const Geo &g) {
+    int o[CV_N];
+    carve_walk(g, o);
     Carve c;
-    carve_walk(g, s, &c);
+    c.t = reinterpret_cast<double *>(s + o[CV_T]); c.pos = reinterpret_cast<float *>(s + o[CV_POS]);
+    c.vel = reinterpret_cast<float *>(s + o[CV_VEL]); c.acc = reinterpret_cast<float *>(s + o[CV_ACC]);
+    c.m = reinterpret_cast<float *>(s + o[CV_M]); c.df = reinterpret_cast<float *>(s + o[CV_DF]);
+    c.inc = reinterpret_cast<uint32_t *>(s + o[CV_INC]); c.x = reinterpret_cast<float *>(s + o[CV_X]);
+    c.nrm = reinterpret_cast<float *>(s + o[CV_NRM]); c.ke = reinterpret_cast<float *>(s + o[CV_KE]);
+    c.pe = reinterpret_cast<float *>(s + o[CV_PE]); c.red = reinterpret_cast<float *>(s + o[CV_RED]);
+    c.moff = reinterpret_cast<int *>(s + o[CV_MOFF]); c.eoff = reinterpret_cast<int *>(s + o[CV_EOFF]);
+    c.uoff = reinterpret_cast<int *>(s + o[CV_UOFF]);
     return c;
 }
 
@@ -1568,9 +1572,14 @@ __device__ __forceinline__ void lean_tile(const wg_batch &b, const KParams &kp, 
 }
 
 // QUO's slice (~12 KB per wave for the canonical walker) holds a CU to ~3 waves per SIMD, so its register
-// budget is the 3-wave one (no spills) instead of the 6-wave one of the default path.
+// budget is the 3-wave one (no spills) instead of the 6-wave one of the default path.  Eight edge passes
+// (NE 8: up to 512 springs per 64 lanes) and the persistent form's prefetch registers do not fit the
+// 6-wave budget either: 4 / 5 waves keep them spill-free (their LDS slices bound occupancy near there).
+constexpr int lean_waves(int NE, bool PERSIST, bool QUO) {
+    return QUO ? 3 : NE >= 8 ? 4 : PERSIST ? 5 : 6;
+}
 template <bool IN3D, int NE, bool PERSIST, bool QUO>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QUO ? 3 : 6))) void walker_step_lean(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lean_waves(NE, PERSIST, QUO)))) void walker_step_lean(
     wg_batch b, KParams kp, const float *__restrict__ action, int action_cols, int action_stride, wg_outputs o,
     LeanGeo lg) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1879,7 +1888,7 @@ int lean_blocks(const wg_batch *b, const LeanGeo &g) {
         int cus = 256, dev = 0;
         if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             cus = 256;
-        const int waves_cu = g.persist == 2 ? 12 : 24;   // VGPR-limited waves per CU: 3 / 6 per SIMD
+        const int waves_cu = g.persist == 2 ? 12 : 20;   // VGPR-limited waves per CU: 3 / 5 per SIMD (lean_waves)
         int per_cu = std::max(1, std::min((160 * 1024 - 4096) / (g.wpb * g.slice), waves_cu / g.wpb));
         per_cu = std::max(1, env_int("WG_LEAN_PER_CU", per_cu));
         blocks = std::min(blocks, per_cu * cus);

@@ -18,13 +18,15 @@ LIB_PATH = os.path.join(HERE, "liboracle.so")
 _i32p = C.POINTER(C.c_int32)
 _f32p = C.POINTER(C.c_float)
 _u8p = C.POINTER(C.c_uint8)
+_f64p = C.POINTER(C.c_double)
 
 
 class OrcParams(C.Structure):
     _fields_ = [(n, C.c_double) for n in ("g", "dampk", "ground", "groundk", "grounddamp", "friction",
                                            "dt", "pk", "vk", "ak", "mk")] + \
                [(n, C.c_int32) for n in ("in3d", "max_steps", "midform", "conmid", "spring_mode",
-                                         "action_mode", "integrator", "pair_mode")] + [("pair_g", C.c_double)]
+                                         "action_mode", "integrator", "pair_mode")] + \
+               [(n, C.c_double) for n in ("pair_g", "pair_k", "pair_e", "bounce_k")]
 
 
 class OrcBatch(C.Structure):
@@ -32,7 +34,8 @@ class OrcBatch(C.Structure):
                 ("pos", _f32p), ("vel", _f32p), ("acc", _f32p), ("m", _f32p),
                 ("ei", _i32p), ("ej", _i32p), ("rest", _f32p), ("k", _f32p), ("c", _f32p),
                 ("flags", _u8p), ("mx", _f32p), ("minl", _f32p), ("maxl", _f32p), ("stride", _f32p),
-                ("steps", _i32p), ("contact", _u8p), ("pinned", _u8p)]
+                ("steps", _i32p), ("contact", _u8p), ("pinned", _u8p),
+                ("charge", _f64p), ("radius", _f64p)]
 
 
 class OrcOut(C.Structure):
@@ -72,7 +75,8 @@ def _p(a, t):
 
 DEFAULT_PARAMS = dict(g=100.0, dampk=0.0, ground=0.0, groundk=1000.0, grounddamp=100.0, friction=100.0,
                       dt=0.01, in3d=1, max_steps=1000, pk=1.0, vk=1.0, ak=1.0, mk=1.0, midform=1,
-                      conmid=0, spring_mode=0, action_mode=0, integrator=1, pair_mode=0, pair_g=9.8)
+                      conmid=0, spring_mode=0, action_mode=0, integrator=1, pair_mode=0, pair_g=9.8,
+                      pair_k=8.99e9, pair_e=16e-20, bounce_k=100.0)
 
 
 class Oracle:
@@ -115,6 +119,12 @@ class Oracle:
         self.contact = np.zeros(len(self.m), np.uint8)
         pin = s.get("pinned")
         self.pinned = None if pin is None or not np.any(pin) else np.ascontiguousarray(pin, np.uint8).copy()
+        # Point.e / Point.r (gym/engine.py:31-50: e = Config.e, r = m ** 0.3 unless given), Python floats
+        ch = s.get("charge")
+        self.charge = None if ch is None else np.ascontiguousarray(ch, np.float64).copy()
+        rad = s.get("radius")
+        self.radius = (self.m.astype(np.float64) ** 0.3 if rad is None
+                       else np.ascontiguousarray(rad, np.float64)).copy()
         self.n_threads = n_threads
         Ms = np.diff(self.mass_off)
         d = 3 if P["in3d"] else 2
@@ -132,7 +142,7 @@ class Oracle:
             _p(self.ei, _i32p), _p(self.ej, _i32p), _p(self.rest, _f32p), _p(self.k, _f32p),
             _p(self.c, _f32p), _p(self.flags, _u8p), _p(self.mx, _f32p), _p(self.minl, _f32p),
             _p(self.maxl, _f32p), _p(self.stride, _f32p), _p(self.steps, _i32p), _p(self.contact, _u8p),
-            _p(self.pinned, _u8p))
+            _p(self.pinned, _u8p), _p(self.charge, _f64p), _p(self.radius, _f64p))
 
     def _outs(self):
         o = dict(obs=np.zeros((self.N, self.obs_stride), np.float32), reward=np.zeros(self.N, np.float32),

@@ -26,7 +26,7 @@
 #include <omp.h>
 #endif
 
-#define ORC_ABI 2
+#define ORC_ABI 3
 int orc_abi_version(void) { return ORC_ABI; }
 
 /* Config.r (gym/engine.py:9, gym/optimized_engine.py:7): the distance clamp, a Python float. */
@@ -170,20 +170,46 @@ static void walker_step(const orc_batch *b, const orc_params *p, int w, const fl
         }
     }
 
-    /* 3b. pair_mode 1: Point.gravity (gym/engine.py:128-137) over this walker's masses.  For each pair i < j:
-     *     r = max(norm(pos_i - pos_j) as float64, Config.r); f = -g * m_i * m_j / r**2 (Python floats);
-     *     j.anti_forced(f, i) then i.anti_forced(f, j) (:69-76): force = -f * direction / distance, all
-     *     float64 (f is a numpy float64 scalar: r came from .astype(float)); forced: a += force / m
-     *     (float64, rounded to float32). */
-    if (p->pair_mode == 1) {
+    /* 3b. pair forces over this walker's own points, after its springs, in the order
+     *     gravity, coulomb, bounce.  Gravity / coulomb, for each pair i < j (gym/engine.py:128-147):
+     *     r = max(norm(pos_i - pos_j) as float64, Config.r); f = -c * q_i * q_j / r**2 (Python floats:
+     *     c, q = Config.g, m or Config.k, e); j.anti_forced(f, i) then i.anti_forced(f, j) (:69-76):
+     *     force = -f * direction / distance, all float64 (f is a numpy float64 scalar: r came from
+     *     .astype(float)); forced: a += force / m (float64, rounded to float32). */
+    for (int pass = 0; pass < 2; pass++) {
+        if (!(p->pair_mode & (1 << pass))) continue;
+        const double cc = pass == 0 ? p->pair_g : p->pair_k;
         for (int i = m0; i < m1; i++)
             for (int j = i + 1; j < m1; j++) {
                 const float *pi = pos + 3 * i, *pj = pos + 3 * j;
                 double r = (double)np_norm3(pi[0] - pj[0], pi[1] - pj[1], pi[2] - pj[2]);
                 if (CONFIG_R > r) r = CONFIG_R;
-                const double f = ((-p->pair_g) * (double)b->m[i]) * (double)b->m[j] / (r * r);
+                const double qi = pass == 0 ? (double)b->m[i] : (b->charge ? b->charge[i] : p->pair_e);
+                const double qj = pass == 0 ? (double)b->m[j] : (b->charge ? b->charge[j] : p->pair_e);
+                const double f = ((-cc) * qi) * qj / (r * r);
                 for (int c = 0; c < 3; c++) acc[3 * j + c] = add_f64(acc[3 * j + c], (-f) * (double)(pi[c] - pj[c]) / r, b->m[j]);
                 for (int c = 0; c < 3; c++) acc[3 * i + c] = add_f64(acc[3 * i + c], (-f) * (double)(pj[c] - pi[c]) / r, b->m[i]);
+            }
+    }
+    /*     Bounce: for s in registry order, for every other point i (gym/engine.py:114-125): if
+     *     norm(s.pos - i.pos).astype(float) <= s.r + i.r: s.resilience(i, s.r + i.r, k / 2) (:78-102),
+     *     a rigid spring of rest x = s.r + i.r (Python float, weakly cast to float32 in dx = current - x)
+     *     and stiffness k/2 (float32 in f_size = -dx * k), applied to s then to i as in the spring pass. */
+    if (p->pair_mode & 4) {
+        const float kb = (float)(p->bounce_k / 2);
+        for (int s = m0; s < m1; s++)
+            for (int i = m0; i < m1; i++) {
+                if (i == s) continue;
+                const float *ps = pos + 3 * s, *pi = pos + 3 * i;
+                const double x = b->radius[s] + b->radius[i];
+                const float cur = np_norm3(ps[0] - pi[0], ps[1] - pi[1], ps[2] - pi[2]);
+                if (!((double)cur <= x)) continue;
+                const float dx = cur - (float)x;
+                const float nf = -((-dx) * kb);
+                double dist = (double)cur;
+                if (CONFIG_R > dist) dist = CONFIG_R;
+                for (int c = 0; c < 3; c++) acc[3 * s + c] = add_f64(acc[3 * s + c], (double)(nf * (pi[c] - ps[c])) / dist, b->m[s]);
+                for (int c = 0; c < 3; c++) acc[3 * i + c] = add_f64(acc[3 * i + c], (double)(nf * (ps[c] - pi[c])) / dist, b->m[i]);
             }
     }
 
@@ -210,6 +236,7 @@ static void walker_step(const orc_batch *b, const orc_params *p, int w, const fl
             a[2] = add_f32(a[2], (-v[2]) * ff, mf);
         }
         if (b->contact) b->contact[q] = (uint8_t)hit;   /* replaces color/r (optimized_env.py:155-175) */
+        if (b->radius) b->radius[q] = hit ? 3.0 : 1.0;  /* p.r = 3 / p.r = 1 (optimized_env.py:156,175) */
         /* DingPoint (gym/optimized_engine.py:404-416): forced() is a no-op, so every force above left
          * its a at the zeros() of step 2; the env then integrates it with the base Point.run1. */
         if (b->pinned && b->pinned[q]) a[0] = a[1] = a[2] = 0.f;

@@ -19,8 +19,13 @@ typedef struct orc_params {
     int32_t spring_mode;   /* 0 = engine.py resilience + G2 damping; 1 = G2 optimized_walker as written */
     int32_t action_mode;   /* 0 = Muscle.act (continuous); 1 = Muscle.actdisp (discrete) */
     int32_t integrator;    /* 0/1 = Point.run1 (gym/engine.py:168-178); 2 = Point.run2 (:180-190) */
-    int32_t pair_mode;     /* 1 = per-walker Point.gravity (gym/engine.py:128-137) after the springs */
-    double pair_g;         /* its Config.g */
+    int32_t pair_mode;     /* bitmask, per walker after the springs, in this order: 1 = Point.gravity
+                              (gym/engine.py:128-137), 2 = Point.coulomb (:139-147), 4 = Point.bounce
+                              for every point in registry order (:114-125) */
+    double pair_g;         /* Config.g of the gravity pass (gym/engine.py:12) */
+    double pair_k;         /* Config.k of the coulomb pass (gym/engine.py:11) */
+    double pair_e;         /* Point.e when charge == NULL (Config.e, gym/engine.py:10) */
+    double bounce_k;       /* Point.bounce(k) (gym/engine.py:114, default 100) */
 } orc_params;
 
 typedef struct orc_batch {
@@ -36,6 +41,10 @@ typedef struct orc_batch {
     int32_t *steps;                  /* [N] */
     uint8_t *contact;                /* [P] (may be NULL) */
     const uint8_t *pinned;           /* [P] 1 = DingPoint, forced() a no-op (may be NULL) */
+    const double *charge;            /* [P] Point.e (Python floats); NULL = pair_e for every point */
+    double *radius;                  /* [P] Point.r (Python floats), read by bounce; the env pass sets
+                                        3 on contact, 1 otherwise (optimized_env.py:156,175); may be NULL
+                                        unless pair_mode & 4 */
 } orc_batch;
 
 typedef struct orc_out {

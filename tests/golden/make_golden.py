@@ -120,8 +120,10 @@ class Spec:
     """A batch in the flat CSR layout used by the oracle and the GPU path."""
 
     def __init__(self, m, pos, vel, mass_off, ei, ej, rest, k, c, flags, edge_off, n_muscles,
-                 minl, maxl, stride, acc=None, pinned=None, mx=None):
+                 minl, maxl, stride, acc=None, pinned=None, mx=None, charge=None, radius=None):
         self.m = np.asarray(m, np.float32)
+        self.charge = None if charge is None else np.asarray(charge, np.float64)   # Point.e
+        self.radius = None if radius is None else np.asarray(radius, np.float64)   # Point.r
         self.pos = np.asarray(pos, np.float32).reshape(-1, 3)
         self.vel = np.asarray(vel, np.float32).reshape(-1, 3)
         self.acc = np.zeros_like(self.pos) if acc is None else np.asarray(acc, np.float32).reshape(-1, 3)
@@ -147,6 +149,9 @@ class Spec:
         for key in ("m", "pos", "vel", "acc", "mass_off", "ei", "ej", "rest", "k", "c", "flags",
                     "edge_off", "n_muscles", "minl", "maxl", "stride"):
             d[prefix + key] = getattr(self, key)
+        for key in ("charge", "radius"):
+            if getattr(self, key) is not None:
+                d[prefix + key] = getattr(self, key)
         if self.pinned.any():
             d[prefix + "pinned"] = self.pinned
         return d
@@ -177,10 +182,12 @@ def spec_from_creatures(creatures, point_index):
 
 
 PARAM_KEYS = ("g", "dampk", "ground", "groundk", "grounddamp", "friction", "dt", "in3d", "max_steps",
-              "pk", "vk", "ak", "mk", "midform", "conmid", "spring_mode", "integrator", "pair_mode", "pair_g")
+              "pk", "vk", "ak", "mk", "midform", "conmid", "spring_mode", "integrator", "pair_mode", "pair_g",
+              "pair_k", "pair_e", "bounce_k")
 DEFAULT_PARAMS = dict(g=100.0, dampk=0.0, ground=0.0, groundk=1000.0, grounddamp=100.0, friction=100.0,
                       dt=0.01, in3d=1, max_steps=1000, pk=1.0, vk=1.0, ak=1.0, mk=1.0, midform=1,
-                      conmid=0, spring_mode=0, integrator=1, pair_mode=0, pair_g=9.8)
+                      conmid=0, spring_mode=0, integrator=1, pair_mode=0, pair_g=9.8,
+                      pair_k=8.99e9, pair_e=16e-20, bounce_k=100.0)
 
 
 class RefRun:
@@ -223,11 +230,17 @@ class RefRun:
                     continue
                 e.p1.resilience(e.p2, e.x, e.k, bool(getattr(e, "_string", 0)))   # gym/engine.py:78
                 OW.Skeleton(e.p1, e.p2, x=e.x, k=0, dampk=e.dampk).run()          # damping only
-            if P["pair_mode"] == 1:                # gym/engine.py:128-137 over this walker's points only
-                saved, g0 = E.Point.points, E.Config.g
-                E.Point.points, E.Config.g = list(cr.phys), P["pair_g"]
-                E.Point.gravity()
-                E.Point.points, E.Config.g = saved, g0
+            if P["pair_mode"]:                     # gym/engine.py:114-147 over this walker's points only
+                saved, g0, k0 = E.Point.points, E.Config.g, E.Config.k
+                E.Point.points, E.Config.g, E.Config.k = list(cr.phys), P["pair_g"], P["pair_k"]
+                if P["pair_mode"] & 1:
+                    E.Point.gravity()              # :128-137
+                if P["pair_mode"] & 2:
+                    E.Point.coulomb()              # :139-147
+                if P["pair_mode"] & 4:
+                    for p in cr.phys:              # :114-125, registry order
+                        p.bounce(P["bounce_k"])
+                E.Point.points, E.Config.g, E.Config.k = saved, g0, k0
             for p in cr.phys:                      # gym/optimized_env.py:146-172 with forces as f32 arrays
                 p.forced(np.array([0, -P["g"], 0], dtype=f32))
                 p.forced(np.asarray(-P["dampk"] * p.v, dtype=f32))
@@ -326,7 +339,8 @@ def pad_obs(obs_list):
 
 def params_array(p):
     # integrator is recorded only where it is not the default, so the older fixtures stay byte-stable
-    keep = lambda k: (k != "integrator" or p[k] != 1) and (k not in ("pair_mode", "pair_g") or p["pair_mode"] != 0)
+    keep = lambda k: (k != "integrator" or p[k] != 1) and (k not in ("pair_mode", "pair_g") or p["pair_mode"] != 0) and \
+        (k not in ("pair_k", "pair_e", "bounce_k") or p["pair_mode"] > 1)
     return {"param_" + k: np.array(p[k]) for k in PARAM_KEYS if keep(k)}
 
 
@@ -345,6 +359,10 @@ def creatures_from_spec(E, OW, spec: Spec):
                 E.Point.points.append(p)
             else:
                 p = E.Point(float(spec.m[q]), spec.pos[q].copy(), spec.vel[q].copy())
+            if spec.charge is not None:
+                p.e = float(spec.charge[q])
+            if spec.radius is not None:
+                p.r = float(spec.radius[q])
             phys.append(p)
         for q, p in zip(range(a, b), phys):
             p.old_a = spec.acc[q].copy()
@@ -563,6 +581,38 @@ def main():
             crs = creatures_from_spec(E, OW, spec)
         acts = rng2.uniform(-1, 1, (60, spec.N, A)).astype(f32)
         run = RefRun(E, OW, OE, crs, dict(in3d=in3d, pair_mode=1, pair_g=pg))
+        save(name, run, spec, 60, acts)
+
+    # P. per-walker coulomb and bounce (gym/engine.py:139-147, :114-125), after the springs (and after gravity
+    #    when combined: pair_mode is a bitmask applied gravity -> coulomb -> bounce), 60 steps.  Coulomb:
+    #    charges U(-3, 3), Config.k raised to 1e4 so the forces matter.  Bounce: the canonical lattice shrunk
+    #    to spacing 4 with initial radii U(1.5, 3) so neighbours collide; after the first env pass the radii
+    #    are the env's 3 (contact) / 1 (optimized_env.py:156,175).
+    def shrunk(seed):
+        sp = canonical_walkers(3, seed=seed)
+        sp["pos"] = (sp["pos"] * np.float32(0.4)).astype(f32)
+        sp["rest"] = (sp["rest"] * np.float32(0.4)).astype(f32)
+        return sp
+    rng3 = np.random.default_rng(77)
+    for name, sp, in3d, A, pm, extra_p, ch, rad in (
+            ("pair_coulomb_canonical", canonical_walkers(3, seed=41), 1, 8, 2, dict(pair_k=1.0e4),
+             rng3.uniform(-3, 3, 48), None),
+            ("pair_bounce_canonical", shrunk(43), 1, 8, 4, dict(bounce_k=2000.0), None, rng3.uniform(1.5, 3.0, 48)),
+            ("pair_all_balance", None, 0, 2, 7, dict(pair_g=5.0e4, pair_k=2.0e5, bounce_k=500.0),
+             rng3.uniform(-2, 2, 8), None)):
+        fresh()
+        if sp is None:
+            crs0 = reference_builders(E, OW, "balance", 2)
+            base = spec_from_creatures(crs0, None)
+            spec = Spec(**{k: getattr(base, k) for k in ("m", "pos", "vel", "mass_off", "ei", "ej", "rest", "k", "c",
+                                                         "flags", "edge_off", "n_muscles", "minl", "maxl",
+                                                         "stride", "acc", "pinned")}, charge=ch, radius=rad)
+            fresh()
+        else:
+            spec = Spec(**sp, charge=ch, radius=rad)
+        crs = creatures_from_spec(E, OW, spec)
+        acts = rng2.uniform(-1, 1, (60, spec.N, A)).astype(f32)
+        run = RefRun(E, OW, OE, crs, dict(in3d=in3d, pair_mode=pm, **extra_p))
         save(name, run, spec, 60, acts)
 
     # M. G1 builders (gym/walker.py:138-353) run from the reference module itself (load_g1_walker), one of

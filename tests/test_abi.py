@@ -52,6 +52,7 @@ int main(void) {
          sizeof(wg_params), sizeof(wg_batch), sizeof(wg_outputs), sizeof(wg_edge), sizeof(wg_launch_info));
   F(wg_batch, pos) F(wg_batch, edges) F(wg_batch, inc_off) F(wg_batch, muscle_bounds) F(wg_batch, contact)
   F(wg_outputs, obs_step) F(wg_outputs, out_step) F(wg_params, in3d) F(wg_params, action_mode) F(wg_params, pair_g)
+  F(wg_params, bounce_k) F(wg_batch, charge) F(wg_batch, radius)
   return 0;
 }
 """)
@@ -89,6 +90,12 @@ def test_errors_without_gpu(lib):
     plan = np.zeros(2, np.int32)
     assert lib.wg_step(C.byref(b), C.byref(p), None, 0, 0, 0, None, 1, plan.ctypes.data_as(C.c_void_p), 1, None) == _lib.WG_EINVAL
     assert b"pair_mode" in lib.wg_last_error()
+    # unknown pair bits, and bounce without the radius array, are refused before any launch
+    b.ragged = 0
+    for pm in (8, 4):
+        p = _lib.WgParams(pair_mode=pm, bounce_k=100.0)
+        assert lib.wg_step(C.byref(b), C.byref(p), None, 0, 0, 0, None, 1, None, 0, None) == _lib.WG_EINVAL
+        assert b"pair_mode" in lib.wg_last_error()
 
 
 def test_plan_ragged_host(lib):

@@ -13,7 +13,7 @@ import threading
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libwalker_hip.so"
 LIB_PATH = os.path.join(HERE, LIB_NAME)
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 WG_EINVAL, WG_ERANGE, WG_EHIP = -1, -2, -3
 
@@ -24,7 +24,8 @@ class WgParams(C.Structure):
     _fields_ = [(n, C.c_double) for n in ("g", "dampk", "ground", "groundk", "grounddamp", "friction", "dt",
                                            "pk", "vk", "ak", "mk")] + \
                [(n, C.c_int32) for n in ("in3d", "max_steps", "midform", "conmid", "spring_mode", "action_mode",
-                                         "integrator", "pair_mode")] + [("pair_g", C.c_double)]
+                                         "integrator", "pair_mode")] + \
+               [(n, C.c_double) for n in ("pair_g", "pair_k", "pair_e", "bounce_k")]
 
 
 class WgBatch(C.Structure):
@@ -35,7 +36,8 @@ class WgBatch(C.Structure):
                 ("edges", _vp),
                 ("inc", _vp), ("inc_off", _vp),
                 ("muscle_x", _vp), ("muscle_bounds", _vp), ("muscle_stride", _vp),
-                ("steps", _vp), ("contact", _vp), ("pinned", _vp)]
+                ("steps", _vp), ("contact", _vp), ("pinned", _vp),
+                ("charge", _vp), ("radius", _vp)]
 
 
 class WgOutputs(C.Structure):

@@ -44,8 +44,12 @@ class EnvParams:
     spring_mode: int = 0          # 0: engine.py resilience + damping; 1: G2 optimized_walker as written
     action_mode: int = 0          # 0: Muscle.act; 1: Muscle.actdisp
     integrator: int = 1           # 1: Point.run1 (what the envs call); 2: Point.run2 (gym/engine.py:180-190)
-    pair_mode: int = 0            # 1: per-walker Point.gravity (gym/engine.py:128-137) after the springs
-    pair_g: float = 9.8           # Config.g of that pass (gym/engine.py:12)
+    pair_mode: int = 0            # bitmask, per walker after the springs: 1 Point.gravity (gym/engine.py:128-137),
+                                  # 2 Point.coulomb (:139-147), 4 Point.bounce (:114-125), in that order
+    pair_g: float = 9.8           # Config.g of the gravity pass (gym/engine.py:12)
+    pair_k: float = 8.99e9        # Config.k of the coulomb pass (gym/engine.py:11)
+    pair_e: float = 16e-20        # Point.e of every point without a spec charge (Config.e, gym/engine.py:10)
+    bounce_k: float = 100.0       # Point.bounce(k) (gym/engine.py:114)
 
     def to_struct(self) -> _lib.WgParams:
         d = asdict(self)
@@ -71,6 +75,8 @@ class BatchedPhysicsEnv:
         self.sigma = float(rand_sigma)
         host = spec_or_layout if isinstance(spec_or_layout, HostLayout) else pack(spec_or_layout)
         self.batch = DeviceBatch(host, device, contact=contact)
+        if int(self.params.pair_mode) & 4:
+            self.batch.enable_radius()
         self.device = device
         self.N = host.N
         self.obs_len = host.obs_len(self.params.in3d, self.params.conmid)
@@ -107,6 +113,8 @@ class BatchedPhysicsEnv:
         if int(self.obs_len.max()) != self.obs_dim:
             self.obs_dim = int(self.obs_len.max())
             self._alloc_outputs()
+        if int(self.params.pair_mode) & 4:
+            self.batch.enable_radius()
         self._pstruct = self.params.to_struct()
 
     def _check_action(self, action):

@@ -76,8 +76,9 @@ struct KParams {
     double g;
     int max_steps, midform, conmid, spring_mode, action_mode;
     int integrator; // 2: Point.run2, otherwise Point.run1
-    int pair_mode;  // 1: per-walker Point.gravity after the springs (lean kernel)
-    double pair_g;
+    int pair_mode;  // bitmask (lean kernel): 1 Point.gravity, 2 Point.coulomb, 4 Point.bounce, after the springs
+    double pair_g, pair_k, pair_e;
+    float bounce_kh;  // float32(k / 2) of Point.bounce(k)
     int stagger;    // diagnostics (WG_STAGGER): blocks with blockIdx % 4 == k idle k*stagger*64 cycles first
 };
 
@@ -692,6 +693,7 @@ __global__ __launch_bounds__(MAXT) void walker_step_kernel(
                       b.pinned && b.pinned[P0 + lp]);
             STAMP(8);
             if (b.contact) b.contact[P0 + lp] = (uint8_t)hit;
+            if (b.radius) b.radius[P0 + lp] = hit ? 3.0 : 1.0;   // gym/optimized_env.py:156,175
             s.pos[3 * lp] = px; s.pos[3 * lp + 1] = py; s.pos[3 * lp + 2] = pz;
             s.vel[3 * lp] = vx; s.vel[3 * lp + 1] = vy; s.vel[3 * lp + 2] = vz;
             if (SHFL) {      // old_a straight from registers (no LDS copy in the register-reduction kernel)
@@ -1094,6 +1096,7 @@ __global__ __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(4, 8))) vo
         if (acts) b.muscle_x[U0 + tid] = x;
         if (is_mass) {
             if (b.contact) b.contact[P0 + tid] = (uint8_t)hit;
+            if (b.radius) b.radius[P0 + tid] = hit ? 3.0 : 1.0;
             if (my_q == 0) {                                          // gym/optimized_env.py:189-248
                 const size_t wg = (size_t)(w0 + my_wl);
                 b.steps[wg] = steps;
@@ -1321,29 +1324,79 @@ __device__ __forceinline__ void end_terms(double t0, double t1, double t2, float
     sqd[slot] = c0; sqd[n2 + slot] = c1; sqd[2 * n2 + slot] = c2;
 }
 
-// pair_mode 1: Point.gravity (gym/engine.py:128-137) restricted to the walker's masses, after its springs
-// (SURVEY §8(f) 3).  Mass q meets its partners in the reference pair loop's order (i < j): ascending
-// partner index.  Per partner: r = max(norm(p_i - p_j) as float64, Config.r); f = -g*m_i*m_j/r**2 in float64
-// (i the lower index); anti_forced (:69-76): force = (-f * (p_partner - p_q)) / r, all float64 (f is a numpy
-// float64 scalar, r came from .astype(float)); forced (:65-67): a = f32(f64(a) + force/m).  Every lane runs the loop (partner state by ds_bpermute); non-mass lanes
-// discard theirs.  IEEE float64 divisions: an opt-in mode, not the headline path.
-__device__ __forceinline__ void pair_gravity(const KParams &kp, const float *p3, float mf, int lane, int M,
+// pair_mode bits 1 / 2: Point.gravity / Point.coulomb (gym/engine.py:128-147) restricted to the walker's
+// masses, after its springs.  Mass q meets its partners in the reference pair loop's order
+// (i < j): ascending partner index.  Per partner: r = max(norm(p_i - p_j) as float64, Config.r);
+// f = -c*s_i*s_j/r**2 in float64 (c, s = Config.g, m or Config.k, e; i the lower index); anti_forced (:69-76):
+// force = (-f * (p_partner - p_q)) / r, all float64 (f is a numpy float64 scalar, r came from .astype(float));
+// forced (:65-67): a = f32(f64(a) + force/m).  Every lane runs the loop (partner state by ds_bpermute);
+// non-mass lanes discard theirs.  IEEE float64 divisions: an opt-in mode, not the headline path.
+__device__ __forceinline__ void pair_central(double coef, double sq, const float *p3, float mf, int lane, int M,
                                              bool is_mass, float &ax, float &ay, float &az) {
     const int gb = lane & ~(M - 1), q = lane & (M - 1);
     const double md = (double)mf;
     for (int pj = 0; pj < M; pj++) {
         const int src = (gb + pj) << 2;
         const float ox = lane_gather(p3[0], src), oy = lane_gather(p3[1], src), oz = lane_gather(p3[2], src);
-        const float om = lane_gather(mf, src);
+        const double os = lane_gather_d(sq, src);
         if (!is_mass || pj == q) continue;
         const float d0 = ox - p3[0], d1 = oy - p3[1], d2 = oz - p3[2];   // partner - self
         double r = (double)np_norm3(d0, d1, d2);      // == norm(p_i - p_j): the squares do not see the sign
         if (CONFIG_R > r) r = CONFIG_R;
-        const double mlo = pj < q ? (double)om : md, mhi = pj < q ? md : (double)om;
-        const double f = ((-kp.pair_g) * mlo) * mhi / (r * r);
+        const double slo = pj < q ? os : sq, shi = pj < q ? sq : os;
+        const double f = ((-coef) * slo) * shi / (r * r);
         ax = (float)((double)ax + ((-f) * (double)d0 / r) / md);
         ay = (float)((double)ay + ((-f) * (double)d1 / r) / md);
         az = (float)((double)az + ((-f) * (double)d2 / r) / md);
+    }
+}
+
+// pair_mode bit 4: Point.bounce(k) (gym/engine.py:114-125) for every point of the walker in registry order:
+// for each other point i, if norm(s.pos - i.pos).astype(float) <= s.r + i.r, s.resilience(i, s.r + i.r, k/2)
+// (:78-102): a spring of rest x = s.r + i.r (weakly cast to float32 in dx = current - x) and stiffness k/2
+// (float32 in f_size = -dx*k), applied to s and then to i.  The term a pair adds to either end does not
+// depend on which end is s (norm and r_s + r_i are symmetric), so mass q receives, in the reference's order:
+// every partner j < q (outer loop at j), then every partner j != q ascending (outer loop at q), then every
+// partner j > q (outer loop at j).  rs = this lane's Point.r (the env pass overwrites it with 3 / 1).
+__device__ __forceinline__ void pair_bounce(float kh, double rs, const float *p3, float mf, int lane, int M,
+                                            bool is_mass, float &ax, float &ay, float &az) {
+    const int gb = lane & ~(M - 1), q = lane & (M - 1);
+    const double md = (double)mf;
+    for (int ph = 0; ph < 3; ph++) {
+        for (int pj = 0; pj < M; pj++) {
+            const int src = (gb + pj) << 2;
+            const float ox = lane_gather(p3[0], src), oy = lane_gather(p3[1], src), oz = lane_gather(p3[2], src);
+            const double orad = lane_gather_d(rs, src);
+            const bool on = ph == 0 ? pj < q : ph == 1 ? pj != q : pj > q;
+            if (!is_mass || !on) continue;
+            const float d0 = ox - p3[0], d1 = oy - p3[1], d2 = oz - p3[2];   // partner - self
+            const float cur = np_norm3(d0, d1, d2);
+            const double x = rs + orad;
+            if (!((double)cur <= x)) continue;
+            const float dx = cur - (float)x;                                  // engine.py:96
+            const float nf = -((-dx) * kh);                                   // -f_size, :75,100
+            double dist = (double)cur;
+            if (CONFIG_R > dist) dist = CONFIG_R;
+            ax = (float)((double)ax + (double)(nf * d0) / dist / md);
+            ay = (float)((double)ay + (double)(nf * d1) / dist / md);
+            az = (float)((double)az + (double)(nf * d2) / dist / md);
+        }
+    }
+}
+
+// The pair passes of one wave (pair_mode != 0): gravity, coulomb, bounce, each over every walker of the wave.
+// Per-mass charges / radii are loaded here, not in lean_load, so the default path carries no extra registers.
+__device__ __forceinline__ void pair_forces(const wg_batch &b, const KParams &kp, const float *p3, float mf,
+                                         uint32_t pl, int lane, int M, bool is_mass, float &ax, float &ay,
+                                         float &az) {
+    if (kp.pair_mode & 1) pair_central(kp.pair_g, (double)mf, p3, mf, lane, M, is_mass, ax, ay, az);
+    if (kp.pair_mode & 2) {
+        const double e = (b.charge && is_mass) ? b.charge[pl] : kp.pair_e;
+        pair_central(kp.pair_k, e, p3, mf, lane, M, is_mass, ax, ay, az);
+    }
+    if (kp.pair_mode & 4) {
+        const double rs = is_mass ? b.radius[pl] : 0.0;
+        pair_bounce(kp.bounce_kh, rs, p3, mf, lane, M, is_mass, ax, ay, az);
     }
 }
 
@@ -1470,9 +1523,10 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
                             az, 0);
         }
     }
-    if (kp.pair_mode == 1) pair_gravity(kp, L.p3, mf, lane, M, is_mass, ax, ay, az);   // every lane (gathers)
+    if (kp.pair_mode) pair_forces(b, kp, L.p3, mf, pl, lane, M, is_mass, ax, ay, az);   // every lane (gathers)
     if (is_mass) {
         mass_tail(kp, mf, (float)ym, L.p3, L.v3, px, py, pz, vx, vy, vz, ax, ay, az, hit, pin);
+        if (b.radius) b.radius[pl] = hit ? 3.0 : 1.0;   // p.r = 3 / p.r = 1 (gym/optimized_env.py:156,175)
         nv = np_norm3(vx, vy, vz);
         ke = mf * (nv * nv);   // numpy's float32 ** 2 is libm powf: may differ by 1 ulp
         pe = (float)((double)mf * kp.g) * (py - kp.ground);
@@ -1669,6 +1723,9 @@ KParams make_kparams(const wg_params &p) {
     k.integrator = p.integrator;
     k.pair_mode = p.pair_mode;
     k.pair_g = p.pair_g;
+    k.pair_k = p.pair_k;
+    k.pair_e = p.pair_e;
+    k.bounce_kh = (float)(p.bounce_k / 2);
     k.dt2 = (float)(p.dt * p.dt);
     static const int stagger = [] { const char *e = getenv("WG_STAGGER"); return e ? atoi(e) : 0; }();
     k.stagger = stagger;
@@ -1963,9 +2020,13 @@ int run(const wg_batch *b, const wg_params *p, const float *action, int32_t cols
     const int blocks = b->ragged ? plan_blocks : (b->N + g.W - 1) / g.W;
     LeanGeo lg{};
     const bool use_lean = step && lean_geo(b, out.obs ? out.obs_stride : 0, &lg, p->spring_mode);
-    if (step && p->pair_mode != 0 && (p->pair_mode != 1 || !use_lean))
-        return fail(WG_EINVAL, "pair_mode %d needs pair_mode 1 on a uniform batch with M | 64 (4 <= M <= 64), "
-                               "spring_mode 0", p->pair_mode);
+    if (step && (p->pair_mode & ~7))
+        return fail(WG_EINVAL, "pair_mode %d: bits 1 (gravity), 2 (coulomb), 4 (bounce) only", p->pair_mode);
+    if (step && p->pair_mode != 0 && !use_lean)
+        return fail(WG_EINVAL, "pair_mode %d needs a uniform batch with M | 64 (4 <= M <= 64), spring_mode 0 "
+                               "(the lean kernel)", p->pair_mode);
+    if (step && (p->pair_mode & 4) && !b->radius)
+        return fail(WG_EINVAL, "pair_mode 4 (bounce) needs the radius array");
     for (int s = 0; s < n_steps; s++) {
         wg_outputs os = out;
         if (os.obs) os.obs += s * os.obs_step;

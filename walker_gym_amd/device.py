@@ -10,7 +10,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .layout import HostLayout
+from .layout import HostLayout, default_radius
 
 
 def _to_dev(a: np.ndarray, device) -> torch.Tensor:
@@ -31,7 +31,7 @@ def _ptr(t: Optional[torch.Tensor]):
 class DeviceBatch:
     """All walker arrays as device tensors (owned here, borrowed by the kernel per launch)."""
 
-    STATE = ("pos", "vel", "acc", "muscle_x", "steps")
+    STATE = ("pos", "vel", "acc", "muscle_x", "steps")   # + radius when kept (Point.bounce)
 
     def __init__(self, host: HostLayout, device: torch.device, contact: bool = True):
         if device.type != "cuda":
@@ -57,6 +57,8 @@ class DeviceBatch:
         self.steps = _to_dev(host.steps, dv)
         self.contact = torch.zeros(self.P, dtype=torch.uint8, device=dv) if contact else None
         self.pinned = _to_dev(host.pinned, dv) if host.pinned is not None else None
+        self.charge = _to_dev(host.charge, dv) if host.charge is not None else None
+        self.radius = None   # allocated by enable_radius(): the step writes it, so only when bounce needs it
         # placeholders so that zero-size arrays still have a valid device pointer
         self._dummy = torch.zeros(16, dtype=torch.float32, device=dv)
         self.plan = None
@@ -71,6 +73,13 @@ class DeviceBatch:
             self.plan = _to_dev(plan[:nb + 1], dv)
             self.plan_blocks = nb
         self.struct = self._make_struct()
+
+    def enable_radius(self) -> None:
+        """Keep Point.r on the device (pair_mode & 4, Point.bounce): the spec's radii or m ** 0.3."""
+        if self.radius is None:
+            r = self.host.radius if self.host.radius is not None else default_radius(self.host.mass)
+            self.radius = _to_dev(r, self.device)
+            self.struct = self._make_struct()
 
     def _p(self, t):
         if t is None:
@@ -90,7 +99,7 @@ class DeviceBatch:
             inc=self._p(self.inc) if self.inc is not None else None, inc_off=self._p(self.inc_off),
             muscle_x=self._p(self.muscle_x), muscle_bounds=self._p(self.muscle_bounds),
             muscle_stride=self._p(self.muscle_stride), steps=self._p(self.steps), contact=self._p(self.contact),
-            pinned=self._p(self.pinned))
+            pinned=self._p(self.pinned), charge=self._p(self.charge), radius=self._p(self.radius))
 
     def launch_geometry(self) -> dict:
         info = _lib.WgLaunchInfo()
@@ -100,8 +109,14 @@ class DeviceBatch:
                     lds_bytes=info.lds_bytes)
 
     def state_dict(self) -> dict:
-        return {k: getattr(self, k).clone() for k in self.STATE}
+        sd = {k: getattr(self, k).clone() for k in self.STATE}
+        if self.radius is not None:
+            sd["radius"] = self.radius.clone()
+        return sd
 
     def load_state_dict(self, sd: dict) -> None:
         for k in self.STATE:
             getattr(self, k).copy_(sd[k])
+        if "radius" in sd:
+            self.enable_radius()
+            self.radius.copy_(sd["radius"])

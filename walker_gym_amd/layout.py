@@ -49,6 +49,8 @@ class HostLayout:
     muscle_stride: np.ndarray
     steps: np.ndarray
     pinned: Optional[np.ndarray] = None   # uint8 [P]: DingPoint masses (None = no pinned mass)
+    charge: Optional[np.ndarray] = None   # float64 [P]: Point.e (None = Config.e for every point)
+    radius: Optional[np.ndarray] = None   # float64 [P]: Point.r (None = m ** 0.3, gym/engine.py:45-46)
     extra: Dict[str, np.ndarray] = field(default_factory=dict)
 
     @property
@@ -165,7 +167,25 @@ def pack(spec: Dict[str, np.ndarray], mx: Optional[np.ndarray] = None, steps: Op
         muscle_stride=np.ascontiguousarray(s["stride"], f32),
         steps=(np.zeros(N, np.int32) if steps is None else np.ascontiguousarray(steps, np.int32).copy()),
         pinned=_pinned(spec, int(mass_off[-1])),
+        charge=_per_mass_f64(spec, "charge", int(mass_off[-1])),
+        radius=_per_mass_f64(spec, "radius", int(mass_off[-1])),
     )
+
+
+def _per_mass_f64(spec, key: str, P: int):
+    """Point.e / Point.r: Python floats in the reference, kept as float64."""
+    a = spec.get(key)
+    if a is None:
+        return None
+    a = np.ascontiguousarray(a, np.float64).reshape(-1)
+    if a.shape[0] != P:
+        raise ValueError(f"{key} has {a.shape[0]} entries for {P} masses")
+    return a.copy()
+
+
+def default_radius(mass: np.ndarray) -> np.ndarray:
+    """Point.__init__ radius r = m ** 0.3 (gym/engine.py:45-46), m the stored float32 mass as a Python float."""
+    return np.asarray(mass, np.float32).astype(np.float64) ** 0.3
 
 
 def _pinned(spec, P: int):

@@ -26,7 +26,10 @@ class OrcParams(C.Structure):
                                            "dt", "pk", "vk", "ak", "mk")] + \
                [(n, C.c_int32) for n in ("in3d", "max_steps", "midform", "conmid", "spring_mode",
                                          "action_mode", "integrator", "pair_mode")] + \
-               [(n, C.c_double) for n in ("pair_g", "pair_k", "pair_e", "bounce_k")]
+               [(n, C.c_double) for n in ("pair_g", "pair_k", "pair_e", "bounce_k")] + \
+               [("g3_gravity", C.c_double * 3)] + \
+               [(n, C.c_double) for n in ("g3_damping", "g3_air", "g3_ground_level", "g3_restitution",
+                                          "g3_friction")] + [("g3_ground", C.c_int32)]
 
 
 class OrcBatch(C.Structure):
@@ -76,7 +79,9 @@ def _p(a, t):
 DEFAULT_PARAMS = dict(g=100.0, dampk=0.0, ground=0.0, groundk=1000.0, grounddamp=100.0, friction=100.0,
                       dt=0.01, in3d=1, max_steps=1000, pk=1.0, vk=1.0, ak=1.0, mk=1.0, midform=1,
                       conmid=0, spring_mode=0, action_mode=0, integrator=1, pair_mode=0, pair_g=9.8,
-                      pair_k=8.99e9, pair_e=16e-20, bounce_k=100.0)
+                      pair_k=8.99e9, pair_e=16e-20, bounce_k=100.0,
+                      g3_gravity=(0.0, -9.8, 0.0), g3_damping=0.99, g3_air=0.01, g3_ground_level=-50.0,
+                      g3_restitution=0.8, g3_friction=0.5, g3_ground=1)
 
 
 class Oracle:
@@ -134,8 +139,10 @@ class Oracle:
 
     def _mk_structs(self):
         P = self.params
-        self._params = OrcParams(**{k: (float(v) if OrcParams._fields_[[f[0] for f in OrcParams._fields_].index(k)][1]
-                                        is C.c_double else int(v)) for k, v in P.items()})
+        types = dict(OrcParams._fields_)
+        self._params = OrcParams(**{k: (float(v) if types[k] is C.c_double else
+                                        types[k](*[float(x) for x in v]) if k == "g3_gravity" else int(v))
+                                    for k, v in P.items()})
         self._batch = OrcBatch(
             self.N, _p(self.mass_off, _i32p), _p(self.edge_off, _i32p), _p(self.muscle_off, _i32p),
             _p(self.pos, _f32p), _p(self.vel, _f32p), _p(self.acc, _f32p), _p(self.m, _f32p),

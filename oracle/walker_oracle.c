@@ -85,6 +85,73 @@ static inline float regulate(float x, float lo, float hi) {
     return x;
 }
 
+/* spring_mode 2: one G3 Environment.update_physics for walker w (gym/optimized_walker/env.py:135-184), the
+ * walker's springs standing for Environment.springs (muscles first, at their Muscle.x rest).  Everything is
+ * float32: core.py's anti_forced takes the distance as float32 (:88), so no float64 enters. */
+static void walker_step_g3(const orc_batch *b, const orc_params *p, int w) {
+    const int m0 = b->mass_off[w], m1 = b->mass_off[w + 1];
+    const int e0 = b->edge_off[w], e1 = b->edge_off[w + 1];
+    const int u0 = b->muscle_off[w], A = b->muscle_off[w + 1] - u0;
+    float *pos = b->pos, *vel = b->vel, *acc = b->acc;
+    const float gv[3] = {(float)p->g3_gravity[0], (float)p->g3_gravity[1], (float)p->g3_gravity[2]};
+    /* zero (:141-142), then gravity point.forced(self.gravity * point.m) on the env's points (:145-146);
+     * DingPoint.zero / forced are no-ops (core.py:269-275): its a stays zeros */
+    for (int q = m0; q < m1; q++) {
+        const float mf = b->m[q];
+        const int pin = b->pinned && b->pinned[q];
+        for (int c = 0; c < 3; c++) acc[3 * q + c] = pin ? 0.f : 0.f + (gv[c] * mf) / mf;
+    }
+    /* springs in list order (:149-150): core.py resilience (:93-122) -> anti_forced (:85-91):
+     * current = norm(self - other) (float32); f_size = -(current - x) * k (0 for a slack string);
+     * distance = max(norm(direction).astype(float32), Config.r); force = -f_size * direction / distance;
+     * forced: a += force / m, all float32 */
+    for (int e = e0; e < e1; e++) {
+        const int i = m0 + b->ei[e], j = m0 + b->ej[e];
+        const float x = (e - e0 < A) ? b->mx[u0 + (e - e0)] : b->rest[e];
+        const float *pi = pos + 3 * i, *pj = pos + 3 * j;
+        const float cur = np_norm3(pi[0] - pj[0], pi[1] - pj[1], pi[2] - pj[2]);
+        const float dx = cur - x;
+        const int string = b->flags ? (b->flags[e] & 1) : 0;
+        const float fsz = (dx < 0.f && string) ? 0.f : (-dx) * b->k[e];
+        const float nf = -fsz;
+        const float dist = (CONFIG_R > (double)cur) ? (float)CONFIG_R : cur;
+        if (!(b->pinned && b->pinned[i]))
+            for (int c = 0; c < 3; c++) acc[3 * i + c] = acc[3 * i + c] + ((nf * (pj[c] - pi[c])) / dist) / b->m[i];
+        if (!(b->pinned && b->pinned[j]))
+            for (int c = 0; c < 3; c++) acc[3 * j + c] = acc[3 * j + c] + ((nf * (pi[c] - pj[c])) / dist) / b->m[j];
+    }
+    const float damp = (float)p->g3_damping, dragc = (float)(-0.5 * p->g3_air), dt = (float)p->dt;
+    const float level = (float)p->g3_ground_level, rest = (float)p->g3_restitution, fr = (float)p->g3_friction;
+    for (int q = m0; q < m1; q++) {
+        float *a = acc + 3 * q, *v = vel + 3 * q, *x = pos + 3 * q;
+        const float mf = b->m[q];
+        const int pin = b->pinned && b->pinned[q];
+        if (!pin) {
+            /* damping v *= damping (:153-154), then air drag (:157-161): speed = norm(v) (float32);
+             * drag = ((-0.5 * air) * speed) * v, the Python float weakly cast to float32 */
+            for (int c = 0; c < 3; c++) v[c] = v[c] * damp;
+            const float coef = dragc * np_norm3(v[0], v[1], v[2]);
+            for (int c = 0; c < 3; c++) a[c] = a[c] + (coef * v[c]) / mf;
+        }
+        /* Point.run1 over the registry, DingPoints included (core.py:185-200): v += a*t; pos += v*t */
+        for (int c = 0; c < 3; c++) v[c] = v[c] + a[c] * dt;
+        for (int c = 0; c < 3; c++) x[c] = x[c] + v[c] * dt;
+        /* ground (:164-178), env points only: clamp, then bounce with restitution and friction */
+        int hit = 0;
+        if (!pin && p->g3_ground && x[1] <= level) {
+            hit = 1;
+            x[1] = level;
+            if (v[1] < 0.f) {
+                v[1] = (-v[1]) * rest;
+                v[0] = v[0] * fr;
+                v[2] = v[2] * fr;
+            }
+        }
+        if (b->contact) b->contact[q] = (uint8_t)hit;
+    }
+    b->steps[w] += 1;
+}
+
 static void walker_step(const orc_batch *b, const orc_params *p, int w, const float *action,
                         int32_t action_cols, int32_t action_stride) {
     const int m0 = b->mass_off[w], m1 = b->mass_off[w + 1];
@@ -105,6 +172,11 @@ static void walker_step(const orc_batch *b, const orc_params *p, int w, const fl
             x = regulate(x, x0 * b->minl[u0 + u], x0 * b->maxl[u0 + u]);
             b->mx[u0 + u] = x;
         }
+    }
+
+    if (p->spring_mode == 2) {            /* the G3 engine instead of steps 2-5 */
+        walker_step_g3(b, p, w);
+        return;
     }
 
     /* 2. zero accelerations (Creature.run, gym/optimized_walker.py:120-121). */

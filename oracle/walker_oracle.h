@@ -16,7 +16,8 @@ typedef struct orc_params {
     double g, dampk, ground, groundk, grounddamp, friction, dt;
     double pk, vk, ak, mk;
     int32_t in3d, max_steps, midform, conmid;
-    int32_t spring_mode;   /* 0 = engine.py resilience + G2 damping; 1 = G2 optimized_walker as written */
+    int32_t spring_mode;   /* 0 = engine.py resilience + G2 damping; 1 = G2 optimized_walker as written;
+                              2 = the G3 engine (optimized_walker/core.py springs, env.py update_physics) */
     int32_t action_mode;   /* 0 = Muscle.act (continuous); 1 = Muscle.actdisp (discrete) */
     int32_t integrator;    /* 0/1 = Point.run1 (gym/engine.py:168-178); 2 = Point.run2 (:180-190) */
     int32_t pair_mode;     /* bitmask, per walker after the springs, in this order: 1 = Point.gravity
@@ -26,6 +27,10 @@ typedef struct orc_params {
     double pair_k;         /* Config.k of the coulomb pass (gym/engine.py:11) */
     double pair_e;         /* Point.e when charge == NULL (Config.e, gym/engine.py:10) */
     double bounce_k;       /* Point.bounce(k) (gym/engine.py:114, default 100) */
+    /* spring_mode 2: the G3 engine, Environment.update_physics (gym/optimized_walker/env.py:135-184) */
+    double g3_gravity[3];  /* Environment.gravity (default (0, -9.8, 0)) */
+    double g3_damping, g3_air, g3_ground_level, g3_restitution, g3_friction;
+    int32_t g3_ground;     /* Environment.ground: the position-clamp ground is on */
 } orc_params;
 
 typedef struct orc_batch {

@@ -673,6 +673,63 @@ def main():
         np.savez_compressed(path, **topo)
         written.append(("g3_builders", os.path.getsize(path)))
 
+    # Q. G3 physics (gym/optimized_walker/env.py:135-184): the reference's own Environment.update_physics run on
+    #    the G3 builders' own points and springs (one batch: every builder, as recorded above), with
+    #    core.Point.run1 over the registry.  Gravity (1, -98, 0) and ground level -20 so the creatures land;
+    #    every third spring a string and random initial velocities so the string and clamp paths both run.
+    #    150 steps.  tests/golden/g3/g3_physics.npz (state only: the G3 env has no observation or reward).
+    g3_names = [("leg2", {}), ("box", {}), ("balance1", {}), ("balance2", {}), ("balance3", {}),
+                ("humanb", {}), ("insect", {}), ("insect8", {"legs": 8})]
+    core.Point.points = []
+    all_pts, all_springs, mass_off, edge_off = [], [], [0], [0]
+    ei, ej, rest, kk, flags = [], [], [], [], []
+    rng4 = np.random.default_rng(91)
+    for n, kw in g3_names:
+        env = EnvRecorder()
+        cr = getattr(g3w, n.rstrip("8") if n == "insect8" else n)(env, **kw)
+        pts = cr.skeleton.points
+        idx = {id(p): q for q, p in enumerate(pts)}
+        for s_i, (a, b_, x, k, st) in enumerate(env.springs):
+            st = bool(s_i % 3 == 2)
+            all_springs.append((a, b_, x, k, st))
+            ei.append(idx[id(a)]); ej.append(idx[id(b_)]); rest.append(np.float32(x)); kk.append(k)
+            flags.append(1 if st else 0)
+        for p in pts:
+            if not isinstance(p, core.DingPoint):
+                p.v[:] = rng4.uniform(-5, 5, 3).astype(f32)
+        all_pts.extend(pts)
+        mass_off.append(len(all_pts)); edge_off.append(len(all_springs))
+    ding = [p for p in all_pts if isinstance(p, core.DingPoint)]
+    shim = types.SimpleNamespace(points=[p for p in all_pts if not isinstance(p, core.DingPoint)], ding_points=ding,
+                                 springs=all_springs, gravity=np.array([1.0, -98.0, 0.0], f32), damping=0.99,
+                                 air_resistance=0.01, ground=True, ground_level=-20.0, ground_restitution=0.8,
+                                 friction=0.5, time_step=0.01, frame_count=0)
+    core.Point.points = list(all_pts)
+    g3in = dict(in_m=np.array([float(p.m) for p in all_pts], f32), in_pos=np.array([p.pos for p in all_pts], f32),
+                in_vel=np.array([p.v for p in all_pts], f32), in_pinned=np.array([isinstance(p, core.DingPoint)
+                                                                                  for p in all_pts], np.uint8),
+                in_mass_off=np.array(mass_off, np.int32), in_edge_off=np.array(edge_off, np.int32),
+                in_ei=np.array(ei, np.int32), in_ej=np.array(ej, np.int32), in_rest=np.array(rest, f32),
+                in_k=np.array(kk, f32), in_c=np.zeros(len(rest), f32), in_flags=np.array(flags, np.uint8),
+                in_n_muscles=np.zeros(len(g3_names), np.int32), in_minl=np.zeros(0, f32),
+                in_maxl=np.zeros(0, f32), in_stride=np.zeros(0, f32),
+                param_g3_gravity=np.array([1.0, -98.0, 0.0]), param_g3_damping=np.array(0.99),
+                param_g3_air=np.array(0.01), param_g3_ground=np.array(1), param_g3_ground_level=np.array(-20.0),
+                param_g3_restitution=np.array(0.8), param_g3_friction=np.array(0.5), param_dt=np.array(0.01),
+                param_spring_mode=np.array(2), param_in3d=np.array(1))
+    outs = {"out_pos": [], "out_vel": [], "out_acc": []}
+    for t in range(150):
+        g3env.Environment.update_physics(shim)
+        outs["out_pos"].append(np.array([p.pos for p in all_pts], f32))
+        outs["out_vel"].append(np.array([p.v for p in all_pts], f32))
+        outs["out_acc"].append(np.array([p.old_a for p in all_pts], f32))
+    if args.only is None or "g3_physics" in args.only:
+        os.makedirs(os.path.join(args.out, "g3"), exist_ok=True)
+        path = os.path.join(args.out, "g3", "g3_physics.npz")
+        np.savez_compressed(path, **g3in, **{k: np.stack(v) for k, v in outs.items()},
+                            g3_names=np.array([n for n, _ in g3_names]), numpy_version=np.array(np.__version__))
+        written.append(("g3_physics", os.path.getsize(path)))
+
     for name, size in written:
         print(f"{name:16s} {size:9d} B")
 

@@ -25,7 +25,10 @@ class WgParams(C.Structure):
                                            "pk", "vk", "ak", "mk")] + \
                [(n, C.c_int32) for n in ("in3d", "max_steps", "midform", "conmid", "spring_mode", "action_mode",
                                          "integrator", "pair_mode")] + \
-               [(n, C.c_double) for n in ("pair_g", "pair_k", "pair_e", "bounce_k")]
+               [(n, C.c_double) for n in ("pair_g", "pair_k", "pair_e", "bounce_k")] + \
+               [("g3_gravity", C.c_double * 3)] + \
+               [(n, C.c_double) for n in ("g3_damping", "g3_air", "g3_ground_level", "g3_restitution",
+                                          "g3_friction")] + [("g3_ground", C.c_int32)]
 
 
 class WgBatch(C.Structure):

@@ -50,6 +50,14 @@ class EnvParams:
     pair_k: float = 8.99e9        # Config.k of the coulomb pass (gym/engine.py:11)
     pair_e: float = 16e-20        # Point.e of every point without a spec charge (Config.e, gym/engine.py:10)
     bounce_k: float = 100.0       # Point.bounce(k) (gym/engine.py:114)
+    # spring_mode 2: the G3 engine (gym/optimized_walker/env.py:10-14 defaults, update_physics :135-184)
+    g3_gravity: tuple = (0.0, -9.8, 0.0)
+    g3_damping: float = 0.99
+    g3_air: float = 0.01
+    g3_ground_level: float = -50.0
+    g3_restitution: float = 0.8
+    g3_friction: float = 0.5
+    g3_ground: int = 1
 
     def to_struct(self) -> _lib.WgParams:
         d = asdict(self)
@@ -57,9 +65,13 @@ class EnvParams:
             d["integrator"] = int(d["integrator"][-1])
         if int(d["integrator"]) not in (0, 1, 2):
             raise ValueError("integrator must be 1 ('run1') or 2 ('run2')")
-        return _lib.WgParams(**{k: (int(v) if k in ("in3d", "max_steps", "midform", "conmid", "spring_mode",
-                                                    "action_mode", "integrator", "pair_mode") else float(v))
-                                for k, v in d.items()})
+        gv = tuple(float(x) for x in d.pop("g3_gravity"))
+        if len(gv) != 3:
+            raise ValueError("g3_gravity must have 3 components")
+        return _lib.WgParams(g3_gravity=(C.c_double * 3)(*gv),
+                             **{k: (int(v) if k in ("in3d", "max_steps", "midform", "conmid", "spring_mode",
+                                                    "action_mode", "integrator", "pair_mode", "g3_ground")
+                                    else float(v)) for k, v in d.items()})
 
 
 class BatchedPhysicsEnv:

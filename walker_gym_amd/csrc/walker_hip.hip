@@ -79,6 +79,9 @@ struct KParams {
     int pair_mode;  // bitmask (lean kernel): 1 Point.gravity, 2 Point.coulomb, 4 Point.bounce, after the springs
     double pair_g, pair_k, pair_e;
     float bounce_kh;  // float32(k / 2) of Point.bounce(k)
+    // spring_mode 2, the G3 engine (gym/optimized_walker/env.py:135-184), everything rounded to float32
+    float g3g[3], g3_damp, g3_dragc, g3_level, g3_rest, g3_fric;   // g3_dragc = f32(-0.5 * air_resistance)
+    int g3_ground;
     int stagger;    // diagnostics (WG_STAGGER): blocks with blockIdx % 4 == k idle k*stagger*64 cycles first
 };
 
@@ -285,6 +288,17 @@ __device__ __forceinline__ void spring_edge(const EdgeRec &e, int le, int lm, fl
     const float cur = np_norm3(pix - pjx, piy - pjy, piz - pjz);   // engine.py:86
     const float dx = cur - x;                                       // engine.py:96
     const float r0 = pjx - pix, r1 = pjy - piy, r2 = pjz - piz;     // other.pos - self.pos
+    if (spring_mode == 2) {
+        // G3 core.py resilience (:93-122) -> anti_forced (:85-91): the distance is float32 (:88), so the
+        // force -f_size * direction / distance stays float32; no damping term.  Cold mode: IEEE divisions.
+        const float fsz = (dx < 0.f && edge_string(e.ij)) ? 0.f : (-dx) * e.k;
+        const float nf = -fsz;
+        const float df = (CONFIG_R > (double)cur) ? (float)CONFIG_R : cur;
+        st[3 * le] = (double)((nf * r0) / df); st[3 * le + 1] = (double)((nf * r1) / df);
+        st[3 * le + 2] = (double)((nf * r2) / df);
+        sdf[3 * le] = 0.f; sdf[3 * le + 1] = 0.f; sdf[3 * le + 2] = 0.f;
+        return;
+    }
     double dist = (double)cur;                                      // engine.py:73
     if (CONFIG_R > dist) dist = CONFIG_R;                           // max(distance, r)
     const double yc = 1.0 / dist;
@@ -457,11 +471,49 @@ __device__ __forceinline__ void mass_accumulate(const double *st, const float *s
     }
 }
 
+// spring_mode 2: one mass of the G3 engine, Environment.update_physics (gym/optimized_walker/env.py:135-184),
+// all float32 with IEEE divisions: a = 0 + (gravity*m)/m (:141-146), the spring terms in edge order
+// (:149-150), v *= damping (:153-154), drag ((-0.5*air)*|v|)*v / m (:157-161), Point.run1 (core.py:185-200),
+// then the position-clamp ground with restitution and friction (:164-178).  A DingPoint (pinned) is not one
+// of the env's points: no force, no damping, no ground, but run1 still moves it by its velocity.
+__device__ __forceinline__ void g3_mass_step(const KParams &kp, const double *st, const uint16_t *inc, int lb, int s0,
+                                          int s1, float mf, const float *p3, const float *v3, float &px, float &py,
+                                          float &pz, float &vx, float &vy, float &vz, float &ax, float &ay,
+                                          float &az, bool &hit, bool pinned) {
+    ax = 0.f; ay = 0.f; az = 0.f;
+    vx = v3[0]; vy = v3[1]; vz = v3[2];
+    if (!pinned) {
+        ax = 0.f + (kp.g3g[0] * mf) / mf; ay = 0.f + (kp.g3g[1] * mf) / mf; az = 0.f + (kp.g3g[2] * mf) / mf;
+        for (int r = s0; r < s1; r++) {
+            const int ent = inc[r];
+            const int le = lb + (ent >> 1);
+            const uint32_t sj = (uint32_t)(ent & 1) << 31;   // end j: direction and term negated exactly
+            ax = ax + fxsign((float)st[3 * le] / mf, sj);
+            ay = ay + fxsign((float)st[3 * le + 1] / mf, sj);
+            az = az + fxsign((float)st[3 * le + 2] / mf, sj);
+        }
+        vx = vx * kp.g3_damp; vy = vy * kp.g3_damp; vz = vz * kp.g3_damp;
+        const float coef = kp.g3_dragc * np_norm3(vx, vy, vz);
+        ax = ax + (coef * vx) / mf; ay = ay + (coef * vy) / mf; az = az + (coef * vz) / mf;
+    }
+    vx = vx + ax * kp.dt; vy = vy + ay * kp.dt; vz = vz + az * kp.dt;
+    px = p3[0] + vx * kp.dt; py = p3[1] + vy * kp.dt; pz = p3[2] + vz * kp.dt;
+    hit = !pinned && kp.g3_ground && py <= kp.g3_level;
+    if (hit) {
+        py = kp.g3_level;
+        if (vy < 0.f) { vy = (-vy) * kp.g3_rest; vx = vx * kp.g3_fric; vz = vz * kp.g3_fric; }
+    }
+}
+
 __device__ __forceinline__ void mass_step(const KParams &kp, const double *st, const float *sdf,
                                           const uint16_t *inc, int lb, int s0, int s1, float mf,
                                           const float *p3, const float *v3, float &px, float &py, float &pz,
                                           float &vx, float &vy, float &vz, float &ax, float &ay, float &az,
                                           bool &hit, int spring_mode, bool pinned) {
+    if (spring_mode == 2) {
+        g3_mass_step(kp, st, inc, lb, s0, s1, mf, p3, v3, px, py, pz, vx, vy, vz, ax, ay, az, hit, pinned);
+        return;
+    }
     mass_accumulate(st, sdf, inc, lb, s0, s1, mf, ax, ay, az, spring_mode);
     const float ymf = (float)(1.0 / (double)mf);
     mass_tail(kp, mf, ymf, p3, v3, px, py, pz, vx, vy, vz, ax, ay, az, hit, pinned);
@@ -1726,6 +1778,13 @@ KParams make_kparams(const wg_params &p) {
     k.pair_k = p.pair_k;
     k.pair_e = p.pair_e;
     k.bounce_kh = (float)(p.bounce_k / 2);
+    for (int i = 0; i < 3; i++) k.g3g[i] = (float)p.g3_gravity[i];
+    k.g3_damp = (float)p.g3_damping;
+    k.g3_dragc = (float)(-0.5 * p.g3_air);
+    k.g3_level = (float)p.g3_ground_level;
+    k.g3_rest = (float)p.g3_restitution;
+    k.g3_fric = (float)p.g3_friction;
+    k.g3_ground = p.g3_ground;
     k.dt2 = (float)(p.dt * p.dt);
     static const int stagger = [] { const char *e = getenv("WG_STAGGER"); return e ? atoi(e) : 0; }();
     k.stagger = stagger;
@@ -2020,6 +2079,8 @@ int run(const wg_batch *b, const wg_params *p, const float *action, int32_t cols
     const int blocks = b->ragged ? plan_blocks : (b->N + g.W - 1) / g.W;
     LeanGeo lg{};
     const bool use_lean = step && lean_geo(b, out.obs ? out.obs_stride : 0, &lg, p->spring_mode);
+    if (p->spring_mode < 0 || p->spring_mode > 2)
+        return fail(WG_EINVAL, "spring_mode %d: 0 (engine.py), 1 (G2 element), 2 (G3 engine) only", p->spring_mode);
     if (step && (p->pair_mode & ~7))
         return fail(WG_EINVAL, "pair_mode %d: bits 1 (gravity), 2 (coulomb), 4 (bounce) only", p->pair_mode);
     if (step && p->pair_mode != 0 && !use_lean)

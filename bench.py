@@ -6,7 +6,9 @@
         --master-port P bench.py --gpus N --steps K --warmup W
 
 A step = one env step (act -> springs -> env forces -> run1 -> obs/reward/done/info) over the rank's
-batch, one kernel launch, with obs/reward/done/info materialised every step.  Inputs (state, topology
+batch, with obs/reward/done/info materialised every step.  The batch is split into 2 contiguous walker
+ranges stepped on 2 HIP streams (BatchedPhysicsEnv.run lanes), one launch per range per step: every walker
+takes every step, and one range's next step fills the GPU while the other's drains.  Inputs (state, topology
 and a distinct U(-1,1) action tensor for every timed step) are resident in HBM before timing starts.
 Weak scaling: each rank owns its own `--walkers` walkers (no data-path collective); at rollout end the
 final observations are gathered with one RCCL all_gather_into_tensor (inside the timed region).
@@ -39,6 +41,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--no-control", action="store_true", help="skip the single-launch (lanes 1) control timing")
     return ap.parse_args()
 
 
@@ -149,6 +152,20 @@ def main():
         dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
     wall_max = float(wall_t.item())
 
+    lanes = env._lanes(None)
+    single_ms = None
+    if rank == 0 and lanes > 1 and not args.no_control:
+        # control: the same kernel as one full-batch launch per step (lanes 1), events on its stream.  This is
+        # the per-dispatch duration a rocprofv3 kernel trace reports (tracing serialises the two streams).
+        n1 = max(20, min(args.steps, 100))
+        env.run(acts[:n1], n1, lanes=1)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        env.run(acts[:n1], n1, lanes=1)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        single_ms = e0.elapsed_time(e1) / n1
+
     if rank == 0:
         D = env.obs_dim
         B = algorithmic_bytes_per_walker_step(M, K, A, D)
@@ -170,16 +187,23 @@ def main():
             "dtype": "f32",
             "data": "synthetic (seeded; SURVEY §8(d) canonical walker; U(-1,1) actions, distinct per step)",
             "config": {"workload": f"{args.workload} walkers, {N} per GPU (M={M}, K={K}, A={A}, obs D={D}), "
-                                   "one fused act+physics+observe launch per env step",
+                                   "one fused act+physics+observe launch per env step per walker range "
+                                   f"({env._lanes(None)} ranges on {env._lanes(None)} streams)",
                        "walkers_per_gpu": N, "total_walkers": world * N, "M": M, "K": K, "A": A, "obs_dim": D,
                        "parallelism": f"dp{world}", "rollout_gather": world > 1 and not args.no_gather,
-                       "launch": geo},
+                       "lanes": env._lanes(None), "launch": geo},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": (tr["hbm_bytes_per_launch"] if tr else None),
                          "bytes_per_walker_step": B, "layout_bytes_per_walker_step": B_layout,
-                         "kernel_ms_per_step_events": round(step_ms, 5)},
+                         "kernel_ms_per_step_events": round(step_ms, 5),
+                         "note": (f"achieved = N*B / event time per step; a step is {lanes} concurrent launches "
+                                  "(one per walker range)" if lanes > 1 else "achieved = N*B / event time per launch")},
         }
+        if single_ms:
+            a1 = B * N / (single_ms * 1e-3) / 1e9
+            line["roofline"]["single_launch"] = {"lanes": 1, "kernel_ms_per_launch_events": round(single_ms, 5),
+                                                 "achieved": round(a1, 1), "frac": round(a1 / HBM_PEAK_GBS, 4)}
         if world == 1 and not args.no_cpu_baseline:
             fn = lambda n: make_spec(args.workload, n, seed=99)[0]
             line["cpu_baseline"] = cpu_baseline(fn, params, A, args.cpu_seconds)

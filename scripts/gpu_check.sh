@@ -16,7 +16,12 @@ step() {  # step <name> <timeout_s> <cmd...>
 step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py --steps 300 --warmup 30
-step rocprof_trace 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 200 --warmup 20 --no-cpu-baseline
+step bench_lanes1 600 env WG_LANES=1 python bench.py --steps 300 --warmup 30 --no-cpu-baseline
+step bench_balance 600 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --workload balance
+step bench_ragged 600 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --workload ragged
+step rocprof_trace 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-control
+step trace_span 60 python scripts/trace_span.py gpurun_out/prof/run_kernel_trace.csv 200
+step rocprof_trace_l1 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_l1 -o run --output-format csv -- python scripts/prof_run.py
 if [ -n "$WG_AB" ]; then  # A/B: barrier kernel vs lean
   step bench_barrier 600 env WG_LEAN=0 python bench.py --steps 300 --warmup 30 --no-cpu-baseline
 fi

@@ -13,6 +13,6 @@ n = int(os.environ.get("WG_N", "65536"))
 steps = int(os.environ.get("WG_STEPS", "30"))
 env = BatchedPhysicsEnv(canonical_walkers(n, seed=0), in3d=1)
 acts = (torch.rand((steps, n, 8), device="cuda") * 2 - 1).contiguous()
-env.run(acts, steps)
+env.run(acts, steps, lanes=1)   # one full-batch launch per step: PMC values per dispatch = per step
 torch.cuda.synchronize()
 print("done", steps, "steps")

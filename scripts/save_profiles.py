@@ -23,6 +23,20 @@ if os.path.exists(stats):
     for r in csv.DictReader(open(stats)):
         if "walker_step" in r["Name"]:
             print(f"rocprof: {r['Name'][:80]}  calls {r['Calls']}  avg {float(r['AverageNs']) / 1e3:.2f} us")
+stats1 = os.path.join(g, "prof_l1", "run_kernel_stats.csv")   # one full-batch launch per step (lanes 1)
+if os.path.exists(stats1):
+    shutil.copy(stats1, os.path.join(out, f"{tag}_kernel_stats_lanes1.csv"))
+span = os.path.join(g, "trace_span.log")
+if os.path.exists(span):
+    lines = [l for l in open(span) if l.startswith("{")]
+    if lines:
+        open(os.path.join(out, f"{tag}_trace_span.json"), "w").write(lines[-1])
+for extra in ("lanes1", "balance", "ragged"):
+    f = os.path.join(g, f"bench_{extra}.log")
+    if os.path.exists(f):
+        lines = [l for l in open(f) if l.startswith("{")]
+        if lines:
+            open(os.path.join(out, f"{tag}_bench_{extra}.json"), "w").write(lines[-1])
 bench = os.path.join(g, "bench.log")
 if os.path.exists(bench):
     lines = [l for l in open(bench) if l.startswith("{")]

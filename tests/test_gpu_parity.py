@@ -263,6 +263,29 @@ def test_rollout_equals_stepwise():
         assert np.array_equal(rw.cpu().numpy(), r[t].cpu().numpy())
 
 
+def test_run_lanes_bit_identical():
+    """run() with the walkers split over 2 / 3 streams (lanes) gives the same bits as one stream."""
+    import torch
+    from walker_gym_amd.batched_env import BatchedPhysicsEnv
+    from walker_gym_amd.synthetic import canonical_walkers
+    N = 10000
+    env = BatchedPhysicsEnv(canonical_walkers(N, seed=3), device="cuda:0", in3d=1)
+    acts = (torch.rand((40, N, 8), generator=torch.Generator(device="cuda:0").manual_seed(3), device="cuda:0")
+            * 2 - 1).contiguous()
+    sd0 = env.batch.state_dict()
+    ref = None
+    for lanes in (1, 2, 3):
+        env.batch.load_state_dict(sd0)
+        env.run(acts, 40, lanes=lanes)
+        torch.cuda.synchronize()
+        got = [t.clone() for t in env.batch.state_dict().values()] + [env.obs.clone(), env.reward.clone(),
+                                                                       env.done.clone(), env.energy.clone()]
+        if ref is None:
+            ref = got
+        else:
+            assert all(torch.equal(a, b) for a, b in zip(ref, got)), lanes
+
+
 def test_kernel_variants_agree(tmp_path):
     """The wave-independent lean kernel (default for uniform M | 64 batches), the workgroup kernel it
     replaced (WG_LEAN=0) and the lean variants (prefetching persistent waves, end quotients formed in the

@@ -12,6 +12,7 @@ for ragged batches (``obs_len`` gives each walker's length).
 from __future__ import annotations
 
 import ctypes as C
+import os
 from dataclasses import dataclass, asdict
 from typing import Optional, Sequence
 
@@ -174,12 +175,15 @@ class BatchedPhysicsEnv:
             self.batch.plan_blocks, self._stream()), "wg_step")
         return obs_out, reward_out, done_out
 
-    def run(self, actions, n_steps: int, info: bool = True):
+    def run(self, actions, n_steps: int, info: bool = True, lanes: Optional[int] = None):
         """Throughput path: n_steps env steps in one C call; step s acts with actions[s % T]
         ([T, N, A] device tensor; T == n_steps or 1) and overwrites obs/reward/done(/info) each step."""
         T, n, cols = actions.shape
         if n != self.N or T not in (1, n_steps) or not actions.is_contiguous():
             raise ValueError("actions must be a contiguous [n_steps or 1, N, A] device tensor")
+        lanes = self._lanes(lanes)
+        if lanes > 1:
+            return self._run_lanes(actions, int(n_steps), info, lanes)
         o = self._outputs(self.obs, self.reward, self.done, self.centroid if info else None,
                           self.energy if info else None)
         _lib.check(_lib.load().wg_step(
@@ -187,6 +191,51 @@ class BatchedPhysicsEnv:
             0 if T == 1 else self.N * cols, C.byref(o), int(n_steps),
             None if self.batch.plan is None else C.c_void_p(self.batch.plan.data_ptr()),
             self.batch.plan_blocks, self._stream()), "wg_step")
+
+    def _lanes(self, lanes: Optional[int]) -> int:
+        """Walker ranges run() steps on separate streams.  Default 2 for uniform batches of >= 8192 walkers:
+        measured on the canonical 65,536-walker bench, 36.5 us/step with 2 ranges against 42.9 with 1 and
+        49.0 with 4 (scripts/lanes_ab.py; bit-identical results).  WG_LANES overrides."""
+        if lanes is None:
+            env = os.environ.get("WG_LANES")
+            lanes = int(env) if env else (2 if self.N >= 8192 else 1)
+        if lanes < 1:
+            raise ValueError("lanes must be >= 1")
+        return 1 if self.batch.ragged or self.N < 64 * lanes else lanes
+
+    def _run_lanes(self, actions, n_steps: int, info: bool, lanes: int):
+        """run() with the walkers split into `lanes` contiguous ranges, each stepped by its own stream: the
+        ranges are independent, so one range's step t + 1 fills the GPU while another's step t drains (the
+        launch tail).  Every walker still takes every step, one launch per step per range; the calling
+        stream waits for all ranges before returning (stream-ordered, no host sync)."""
+        T, n, cols = actions.shape
+        cur = torch.cuda.current_stream(self.device)
+        if len(getattr(self, "_side", ())) < lanes - 1:
+            self._side = [torch.cuda.Stream(device=self.device) for _ in range(lanes - 1)]
+        start = torch.cuda.Event()
+        start.record(cur)
+        bounds = [0] + [((self.N * i // lanes) + 63) // 64 * 64 for i in range(1, lanes)] + [self.N]
+        D, L = self.obs_dim, _lib.load()
+        done = []
+        for i in range(lanes):
+            w0, w1 = bounds[i], bounds[i + 1]
+            st = cur if i == 0 else self._side[i - 1]
+            if i:
+                st.wait_event(start)
+            sub = self.batch.sub_struct(w0, w1)
+            o = self._outputs(self.obs[w0:w1], self.reward[w0:w1], self.done[w0:w1],
+                              self.centroid[w0:w1] if info else None, self.energy[w0:w1] if info else None)
+            o.obs_stride = D
+            act = C.c_void_p(actions.data_ptr() + 4 * w0 * cols)
+            _lib.check(L.wg_step(C.byref(sub), C.byref(self._pstruct), act, cols, cols,
+                                 0 if T == 1 else self.N * cols, C.byref(o), n_steps, None, 0,
+                                 C.c_void_p(st.cuda_stream)), "wg_step")
+            if i:
+                ev = torch.cuda.Event()
+                ev.record(st)
+                done.append(ev)
+        for ev in done:
+            cur.wait_event(ev)
 
     def observe(self):
         o = self._outputs(self.obs, self.reward, self.done, self.centroid, self.energy)

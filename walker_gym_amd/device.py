@@ -101,6 +101,30 @@ class DeviceBatch:
             muscle_stride=self._p(self.muscle_stride), steps=self._p(self.steps), contact=self._p(self.contact),
             pinned=self._p(self.pinned), charge=self._p(self.charge), radius=self._p(self.radius))
 
+    def sub_struct(self, w0: int, w1: int) -> _lib.WgBatch:
+        """A WgBatch view of walkers [w0, w1) of a uniform batch: the same device memory, pointers offset
+        (every array is walker-major).  Used to run disjoint walker ranges on separate streams."""
+        if self.ragged:
+            raise ValueError("sub_struct: uniform batches only")
+        if not 0 <= w0 < w1 <= self.N:
+            raise ValueError(f"sub_struct: bad walker range [{w0}, {w1})")
+        M, K, A = self.M, self.K, self.A
+
+        def off(t, elems):
+            return None if t is None else C.c_void_p(t.data_ptr() + elems * t.element_size())
+
+        return _lib.WgBatch(
+            N=w1 - w0, M=M, K=K, A=A, ragged=0, mass_off=None, edge_off=None, muscle_off=None,
+            pos=off(self.pos, 3 * M * w0), vel=off(self.vel, 3 * M * w0), acc=off(self.acc, 3 * M * w0),
+            mass=off(self.mass, M * w0), edges=off(self.edges, 4 * K * w0),
+            inc=off(self.inc, 2 * K * w0) if self.inc is not None else None,
+            inc_off=off(self.inc_off, (M + 1) * w0),
+            muscle_x=self._p(self.muscle_x) if A == 0 else off(self.muscle_x, A * w0),
+            muscle_bounds=self._p(self.muscle_bounds) if A == 0 else off(self.muscle_bounds, 2 * A * w0),
+            muscle_stride=self._p(self.muscle_stride) if A == 0 else off(self.muscle_stride, A * w0),
+            steps=off(self.steps, w0), contact=off(self.contact, M * w0), pinned=off(self.pinned, M * w0),
+            charge=off(self.charge, M * w0), radius=off(self.radius, M * w0))
+
     def launch_geometry(self) -> dict:
         info = _lib.WgLaunchInfo()
         _lib.check(_lib.load().wg_launch_geometry(C.byref(self.struct), C.byref(info)), "wg_launch_geometry")

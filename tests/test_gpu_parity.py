@@ -284,6 +284,13 @@ def test_run_lanes_bit_identical():
             ref = got
         else:
             assert all(torch.equal(a, b) for a, b in zip(ref, got)), lanes
+    # rollout(): per-step outputs of every range land in the right rows
+    outs = []
+    for lanes in (1, 2):
+        env.batch.load_state_dict(sd0)
+        outs.append([t.clone() for t in env.rollout(acts[:12], lanes=lanes)])
+    torch.cuda.synchronize()
+    assert all(torch.equal(a, b) for a, b in zip(*outs))
 
 
 def test_kernel_variants_agree(tmp_path):

@@ -154,7 +154,7 @@ class BatchedPhysicsEnv:
                              self.batch.plan_blocks, self._stream()), "wg_step")
         return self.obs, self.reward, self.done.bool(), self.info()
 
-    def rollout(self, actions, obs_out=None, reward_out=None, done_out=None):
+    def rollout(self, actions, obs_out=None, reward_out=None, done_out=None, lanes: Optional[int] = None):
         """T steps in one C call (T back-to-back launches, no host sync); outputs for every step."""
         if not isinstance(actions, torch.Tensor):
             actions = torch.as_tensor(np.asarray(actions, dtype=np.float32))
@@ -166,6 +166,15 @@ class BatchedPhysicsEnv:
         obs_out = torch.empty((T, self.N, self.obs_dim), dtype=torch.float32, device=dv) if obs_out is None else obs_out
         reward_out = torch.empty((T, self.N), dtype=torch.float32, device=dv) if reward_out is None else reward_out
         done_out = torch.empty((T, self.N), dtype=torch.uint8, device=dv) if done_out is None else done_out
+        if tuple(obs_out.shape) != (T, self.N, self.obs_dim) or tuple(reward_out.shape) != (T, self.N) or \
+                tuple(done_out.shape) != (T, self.N):
+            raise ValueError("rollout outputs must be [T, N, D] / [T, N] / [T, N]")
+        lanes = self._lanes(lanes)
+        if lanes > 1:
+            self._run_lanes(actions, T, lambda w0, w1: self._outputs(
+                obs_out[0, w0:w1], reward_out[0, w0:w1], done_out[0, w0:w1], None, None,
+                obs_step=self.N * self.obs_dim, out_step=self.N), lanes)
+            return obs_out, reward_out, done_out
         o = self._outputs(obs_out, reward_out, done_out, None, None, obs_step=self.N * self.obs_dim,
                           out_step=self.N)
         _lib.check(_lib.load().wg_step(
@@ -183,7 +192,9 @@ class BatchedPhysicsEnv:
             raise ValueError("actions must be a contiguous [n_steps or 1, N, A] device tensor")
         lanes = self._lanes(lanes)
         if lanes > 1:
-            return self._run_lanes(actions, int(n_steps), info, lanes)
+            return self._run_lanes(actions, int(n_steps), lambda w0, w1: self._outputs(
+                self.obs[w0:w1], self.reward[w0:w1], self.done[w0:w1], self.centroid[w0:w1] if info else None,
+                self.energy[w0:w1] if info else None), lanes)
         o = self._outputs(self.obs, self.reward, self.done, self.centroid if info else None,
                           self.energy if info else None)
         _lib.check(_lib.load().wg_step(
@@ -203,11 +214,12 @@ class BatchedPhysicsEnv:
             raise ValueError("lanes must be >= 1")
         return 1 if self.batch.ragged or self.N < 64 * lanes else lanes
 
-    def _run_lanes(self, actions, n_steps: int, info: bool, lanes: int):
-        """run() with the walkers split into `lanes` contiguous ranges, each stepped by its own stream: the
+    def _run_lanes(self, actions, n_steps: int, outputs, lanes: int):
+        """n_steps with the walkers split into `lanes` contiguous ranges, each stepped by its own stream: the
         ranges are independent, so one range's step t + 1 fills the GPU while another's step t drains (the
         launch tail).  Every walker still takes every step, one launch per step per range; the calling
-        stream waits for all ranges before returning (stream-ordered, no host sync)."""
+        stream waits for all ranges before returning (stream-ordered, no host sync).  outputs(w0, w1) gives
+        the WgOutputs of walkers [w0, w1)."""
         T, n, cols = actions.shape
         cur = torch.cuda.current_stream(self.device)
         if len(getattr(self, "_side", ())) < lanes - 1:
@@ -215,7 +227,7 @@ class BatchedPhysicsEnv:
         start = torch.cuda.Event()
         start.record(cur)
         bounds = [0] + [((self.N * i // lanes) + 63) // 64 * 64 for i in range(1, lanes)] + [self.N]
-        D, L = self.obs_dim, _lib.load()
+        L = _lib.load()
         done = []
         for i in range(lanes):
             w0, w1 = bounds[i], bounds[i + 1]
@@ -223,9 +235,7 @@ class BatchedPhysicsEnv:
             if i:
                 st.wait_event(start)
             sub = self.batch.sub_struct(w0, w1)
-            o = self._outputs(self.obs[w0:w1], self.reward[w0:w1], self.done[w0:w1],
-                              self.centroid[w0:w1] if info else None, self.energy[w0:w1] if info else None)
-            o.obs_stride = D
+            o = outputs(w0, w1)
             act = C.c_void_p(actions.data_ptr() + 4 * w0 * cols)
             _lib.check(L.wg_step(C.byref(sub), C.byref(self._pstruct), act, cols, cols,
                                  0 if T == 1 else self.N * cols, C.byref(o), n_steps, None, 0,

@@ -99,6 +99,7 @@ def creatures_to_spec(creatures: List[Creature]) -> dict:
     m, pos, vel, acc, mass_off = [], [], [], [], [0]
     ei, ej, rest, k, c, flags, edge_off = [], [], [], [], [], [], [0]
     nmus, minl, maxl, stride, mx, pinned = [], [], [], [], [], []
+    charge, radius = [], []   # Point.e / Point.r (gym/engine.py:31-50), Python floats: pair_mode coulomb / bounce
     for cr in creatures:
         local = {}
         for p in cr.phys:
@@ -108,6 +109,7 @@ def creatures_to_spec(creatures: List[Creature]) -> dict:
             m.append(float(p.m)); pos.append(np.asarray(p.pos, f32)); vel.append(np.asarray(p.v, f32))
             acc.append(np.asarray(p.old_a, f32))
             pinned.append(1 if isinstance(p, DingPoint) else 0)
+            charge.append(float(getattr(p, "e", 16e-20))); radius.append(float(getattr(p, "r", float(p.m) ** 0.3)))
         mass_off.append(len(m))
         for e in list(cr.muscles) + list(cr.skeletons):
             if id(e.p1) not in local or id(e.p2) not in local:
@@ -126,7 +128,8 @@ def creatures_to_spec(creatures: List[Creature]) -> dict:
                 k=np.array(k, f32), c=np.array(c, f32), flags=np.array(flags, np.uint8),
                 edge_off=np.array(edge_off, np.int32), n_muscles=np.array(nmus, np.int32),
                 minl=np.array(minl, f32), maxl=np.array(maxl, f32), stride=np.array(stride, f32),
-                mx=np.array(mx, f32), pinned=np.array(pinned, np.uint8))
+                mx=np.array(mx, f32), pinned=np.array(pinned, np.uint8),
+                charge=np.array(charge, np.float64), radius=np.array(radius, np.float64))
 
 
 def replicate_spec(spec: dict, n: int) -> dict:
@@ -136,7 +139,7 @@ def replicate_spec(spec: dict, n: int) -> dict:
         raise ValueError("replicate_spec expects a single walker")
     out = {}
     for key in ("m", "pos", "vel", "acc", "ei", "ej", "rest", "k", "c", "flags", "minl", "maxl", "stride", "mx",
-                "pinned"):
+                "pinned", "charge", "radius"):
         if key in spec:
             a = np.asarray(spec[key])
             out[key] = np.tile(a, (n,) + (1,) * (a.ndim - 1))

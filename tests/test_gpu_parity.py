@@ -284,6 +284,20 @@ def test_run_lanes_bit_identical():
             ref = got
         else:
             assert all(torch.equal(a, b) for a, b in zip(ref, got)), lanes
+    # ragged batch: ranges of plan blocks
+    from walker_gym_amd.synthetic import ragged_walkers
+    rg = BatchedPhysicsEnv(ragged_walkers(20000, seed=4, string_frac=0.2), device="cuda:0", in3d=1)
+    assert rg._lanes(2) == 2, rg.batch.plan_blocks
+    ra = (torch.rand((20, 20000, int(rg.batch.A)), generator=torch.Generator(device="cuda:0").manual_seed(4),
+                     device="cuda:0") * 2 - 1).contiguous()
+    rsd = rg.batch.state_dict()
+    rres = []
+    for lanes in (1, 2):
+        rg.batch.load_state_dict(rsd)
+        rg.run(ra, 20, lanes=lanes)
+        torch.cuda.synchronize()
+        rres.append([t.clone() for t in rg.batch.state_dict().values()] + [rg.obs.clone(), rg.reward.clone()])
+    assert all(torch.equal(a, b) for a, b in zip(*rres))
     # rollout(): per-step outputs of every range land in the right rows
     outs = []
     for lanes in (1, 2):

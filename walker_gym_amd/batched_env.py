@@ -204,7 +204,8 @@ class BatchedPhysicsEnv:
             self.batch.plan_blocks, self._stream()), "wg_step")
 
     def _lanes(self, lanes: Optional[int]) -> int:
-        """Walker ranges run() steps on separate streams.  Default 2 for uniform batches of >= 8192 walkers:
+        """Walker ranges run() steps on separate streams (ragged batches: ranges of plan blocks).  Default 2 for
+        batches of >= 8192 walkers:
         measured on the canonical 65,536-walker bench, 36.5 us/step with 2 ranges against 42.9 with 1 and
         49.0 with 4 (scripts/lanes_ab.py; bit-identical results).  WG_LANES overrides."""
         if lanes is None:
@@ -212,7 +213,9 @@ class BatchedPhysicsEnv:
             lanes = int(env) if env else (2 if self.N >= 8192 else 1)
         if lanes < 1:
             raise ValueError("lanes must be >= 1")
-        return 1 if self.batch.ragged or self.N < 64 * lanes else lanes
+        if self.batch.ragged:
+            return max(1, min(lanes, self.batch.plan_blocks // 64))
+        return 1 if self.N < 64 * lanes else lanes
 
     def _run_lanes(self, actions, n_steps: int, outputs, lanes: int):
         """n_steps with the walkers split into `lanes` contiguous ranges, each stepped by its own stream: the
@@ -226,19 +229,27 @@ class BatchedPhysicsEnv:
             self._side = [torch.cuda.Stream(device=self.device) for _ in range(lanes - 1)]
         start = torch.cuda.Event()
         start.record(cur)
-        bounds = [0] + [((self.N * i // lanes) + 63) // 64 * 64 for i in range(1, lanes)] + [self.N]
         L = _lib.load()
+        ragged = self.batch.ragged
+        if ragged:   # ranges of plan blocks: the same batch, a slice of its block -> walker plan
+            nb = self.batch.plan_blocks
+            bounds = [nb * i // lanes for i in range(lanes)] + [nb]
+        else:
+            bounds = [0] + [((self.N * i // lanes) + 63) // 64 * 64 for i in range(1, lanes)] + [self.N]
         done = []
         for i in range(lanes):
             w0, w1 = bounds[i], bounds[i + 1]
             st = cur if i == 0 else self._side[i - 1]
             if i:
                 st.wait_event(start)
-            sub = self.batch.sub_struct(w0, w1)
-            o = outputs(w0, w1)
-            act = C.c_void_p(actions.data_ptr() + 4 * w0 * cols)
+            if ragged:
+                sub, o, act = self.batch.struct, outputs(0, self.N), C.c_void_p(actions.data_ptr())
+                plan, nblk = C.c_void_p(self.batch.plan.data_ptr() + 4 * w0), w1 - w0
+            else:
+                sub, o = self.batch.sub_struct(w0, w1), outputs(w0, w1)
+                act, plan, nblk = C.c_void_p(actions.data_ptr() + 4 * w0 * cols), None, 0
             _lib.check(L.wg_step(C.byref(sub), C.byref(self._pstruct), act, cols, cols,
-                                 0 if T == 1 else self.N * cols, C.byref(o), n_steps, None, 0,
+                                 0 if T == 1 else self.N * cols, C.byref(o), n_steps, plan, nblk,
                                  C.c_void_p(st.cuda_stream)), "wg_step")
             if i:
                 ev = torch.cuda.Event()

@@ -180,6 +180,27 @@ def test_pair_forces_4096_vs_oracle():
     assert np.isfinite(orc.pos).all(1).mean() > 0.95
 
 
+@pytest.mark.parametrize("case", ["M64_K160", "M4_K6", "M16_partial_tile", "M64_K300_NE5", "ragged_M256"])
+def test_size_extremes_vs_oracle(case):
+    """Edges of the launch geometry against the oracle: the largest lean tile (M = 64, one walker per wave,
+    3 and 5 edge passes), the smallest (M = 4, 16 walkers per wave), a batch that ends mid-wave, and ragged
+    walkers up to M = 256 on the workgroup kernel."""
+    from walker_gym_amd.synthetic import canonical_walkers, ragged_walkers
+    if case == "M64_K160":
+        spec, A, N = canonical_walkers(96, seed=11, M=64, K=160, A=20), 20, 96
+    elif case == "M64_K300_NE5":
+        spec, A, N = canonical_walkers(64, seed=12, M=64, K=300, A=8), 8, 64
+    elif case == "M4_K6":
+        spec, A, N = canonical_walkers(1000, seed=13, M=4, K=6, A=2), 2, 1000
+    elif case == "M16_partial_tile":
+        spec, A, N = canonical_walkers(4097, seed=14), 8, 4097
+    else:
+        spec = ragged_walkers(300, seed=15, mmin=100, mmax=256, string_frac=0.1)
+        N, A = 300, int(np.max(spec["n_muscles"]))
+    acts = np.random.default_rng(11).uniform(-1, 1, (8, N, A)).astype(np.float32)
+    _oracle_compare(spec, dict(in3d=1), 8, acts)
+
+
 def test_full_size_sampled_vs_oracle():
     """BASELINE config 3 size (65,536 canonical walkers): walkers are independent, so the oracle
     checks a sample of them (first, last and random walkers) after 10 full-batch GPU steps."""

@@ -24,11 +24,16 @@ VARIANTS = {
     "lean_w2": {"WG_LEAN_WAVES": "2"},
     "lean_w1": {"WG_LEAN_WAVES": "1"},
     "L1": {"WG_LANES": "1"},
+    "prio0": {"WG_LEAN_PRIO": "0"},
+    "prio1": {"WG_LEAN_PRIO": "1"},
+    "prio2": {"WG_LEAN_PRIO": "2"},
+    "prio1_L1": {"WG_LEAN_PRIO": "1", "WG_LANES": "1"},
+    "prio2_L1": {"WG_LEAN_PRIO": "2", "WG_LANES": "1"},
     "L3": {"WG_LANES": "3"},
     "w2_L3": {"WG_LEAN_WAVES": "2", "WG_LANES": "3"},
     "w1_L4": {"WG_LEAN_WAVES": "1", "WG_LANES": "4"},
 }
-KEYS = ("WG_LEAN_PERSIST", "WG_LEAN_QUO", "WG_LEAN_WAVES", "WG_LEAN_PER_CU", "WG_LEAN_BLOCKS", "WG_LANES")
+KEYS = ("WG_LEAN_PERSIST", "WG_LEAN_QUO", "WG_LEAN_WAVES", "WG_LEAN_PER_CU", "WG_LEAN_BLOCKS", "WG_LANES", "WG_LEAN_PRIO")
 
 
 def main():

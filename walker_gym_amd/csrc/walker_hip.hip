@@ -82,6 +82,9 @@ struct KParams {
     // spring_mode 2, the G3 engine (gym/optimized_walker/env.py:135-184), everything rounded to float32
     float g3g[3], g3_damp, g3_dragc, g3_level, g3_rest, g3_fric;   // g3_dragc = f32(-0.5 * air_resistance)
     int g3_ground;
+    int prio;         // WG_LEAN_PRIO: 1 (default) raise the wave priority while a lean tile issues its loads, so a
+                      // wave's HBM requests leave before other waves' arithmetic; 0 off; 2 (experiment) raise it
+                      // from the loads to the end of the tile (oldest first).  scripts/lean_ab.py, DESIGN §7
     int stagger;    // diagnostics (WG_STAGGER): blocks with blockIdx % 4 == k idle k*stagger*64 cycles first
 };
 
@@ -1673,7 +1676,10 @@ __device__ __forceinline__ void lean_tile(const wg_batch &b, const KParams &kp, 
                                           char *sl, int tile, int lane) {
     const LeanTile t = lean_tile_of(b, action, action_cols, lg, tile, lane);
     LeanIn<NE> L;
+    if (kp.prio == 1) __builtin_amdgcn_s_setprio(2);
     lean_load<NE>(b, kp, action, action_stride, t, lane, L);
+    if (kp.prio == 1) __builtin_amdgcn_s_setprio(0);
+    if (kp.prio == 2) __builtin_amdgcn_s_setprio(2);
     lean_compute<IN3D, NE, QUO>(b, kp, o, lg, sl, t, lane, L);
 }
 
@@ -1758,6 +1764,8 @@ __global__ void walker_reset_kernel(wg_batch b, const float *__restrict__ noise,
 }
 
 // ------------------------------------------------------------------ host side
+int env_int(const char *name, int dflt);
+
 KParams make_kparams(const wg_params &p) {
     KParams k;
     k.neg_g = (float)(-p.g);
@@ -1785,6 +1793,7 @@ KParams make_kparams(const wg_params &p) {
     k.g3_rest = (float)p.g3_restitution;
     k.g3_fric = (float)p.g3_friction;
     k.g3_ground = p.g3_ground;
+    k.prio = env_int("WG_LEAN_PRIO", 1);
     k.dt2 = (float)(p.dt * p.dt);
     static const int stagger = [] { const char *e = getenv("WG_STAGGER"); return e ? atoi(e) : 0; }();
     k.stagger = stagger;

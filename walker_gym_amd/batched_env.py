@@ -169,7 +169,7 @@ class BatchedPhysicsEnv:
         if tuple(obs_out.shape) != (T, self.N, self.obs_dim) or tuple(reward_out.shape) != (T, self.N) or \
                 tuple(done_out.shape) != (T, self.N):
             raise ValueError("rollout outputs must be [T, N, D] / [T, N] / [T, N]")
-        lanes = self._lanes(lanes)
+        lanes = self._lanes(lanes) if T > 0 else 1
         if lanes > 1:
             self._run_lanes(actions, T, lambda w0, w1: self._outputs(
                 obs_out[0, w0:w1], reward_out[0, w0:w1], done_out[0, w0:w1], None, None,

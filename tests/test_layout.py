@@ -62,3 +62,35 @@ def test_algorithmic_bytes_canonical():
     # canonical M=16, K=40, A=8, 3-D obs (152 floats) -> 2,440 B per walker-step
     assert algorithmic_bytes_per_walker_step(16, 40, 8, 152) == 2440
     assert algorithmic_bytes_per_walker_step(4, 5, 2, 38) == 536
+
+
+def test_pair_and_g3_host_plumbing():
+    """Point.e / Point.r reach the packed layout (float64, the reference's Python floats); the G3 and pair
+    parameters reach the C struct; a malformed per-mass array is refused."""
+    import ctypes as C
+
+    import pytest
+
+    from walker_gym_amd.batched_env import EnvParams
+    from walker_gym_amd.distributed import shard_spec
+    from walker_gym_amd.layout import default_radius
+    cr = create_balance_creature()
+    cr.phys[1].e = 2.5
+    spec = creatures_to_spec([cr])
+    h = pack(spec)
+    assert h.charge.dtype == np.float64 and h.charge[1] == 2.5 and h.charge[0] == 16e-20
+    assert np.array_equal(h.radius, np.array([float(p.m) ** 0.3 for p in cr.phys]))
+    assert np.array_equal(default_radius(h.mass), h.radius)
+    two = creatures_to_spec([create_balance_creature(), cr])
+    sh = shard_spec(two, 1, 2)
+    assert np.array_equal(sh["charge"], spec["charge"]) and np.array_equal(sh["radius"], spec["radius"])
+    bad = dict(spec)
+    bad["charge"] = spec["charge"][:2]
+    with pytest.raises(ValueError):
+        pack(bad)
+    s = EnvParams(spring_mode=2, g3_gravity=(1.0, -98.0, 0.5), g3_ground=0, pair_mode=6, bounce_k=40.0).to_struct()
+    assert tuple(s.g3_gravity) == (1.0, -98.0, 0.5) and s.g3_ground == 0 and s.spring_mode == 2
+    assert s.pair_mode == 6 and s.bounce_k == 40.0 and s.pair_k == 8.99e9 and s.pair_e == 16e-20
+    assert C.sizeof(s) > 0
+    with pytest.raises(ValueError):
+        EnvParams(g3_gravity=(0.0, 1.0)).to_struct()

@@ -225,8 +225,11 @@ class BatchedPhysicsEnv:
         the WgOutputs of walkers [w0, w1)."""
         T, n, cols = actions.shape
         cur = torch.cuda.current_stream(self.device)
-        if len(getattr(self, "_side", ())) < lanes - 1:
-            self._side = [torch.cuda.Stream(device=self.device) for _ in range(lanes - 1)]
+        prio = int(os.environ.get("WG_LANES_PRIO", "0"))   # experiments: side-stream priority (torch: -1 high)
+        key = (lanes, prio)
+        if getattr(self, "_side_key", None) != key:
+            self._side = [torch.cuda.Stream(device=self.device, priority=prio) for _ in range(lanes - 1)]
+            self._side_key = key
         start = torch.cuda.Event()
         start.record(cur)
         L = _lib.load()

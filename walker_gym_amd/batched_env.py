@@ -255,6 +255,7 @@ class BatchedPhysicsEnv:
                                  0 if T == 1 else self.N * cols, C.byref(o), n_steps, plan, nblk,
                                  C.c_void_p(st.cuda_stream)), "wg_step")
             if i:
+                actions.record_stream(st)   # the allocator must not recycle it before the side stream is done
                 ev = torch.cuda.Event()
                 ev.record(st)
                 done.append(ev)

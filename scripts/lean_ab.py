@@ -24,6 +24,9 @@ VARIANTS = {
     "lean_w2": {"WG_LEAN_WAVES": "2"},
     "lean_w1": {"WG_LEAN_WAVES": "1"},
     "L1": {"WG_LANES": "1"},
+    "split40": {"WG_LANES_SPLIT": "0.4"},
+    "split30": {"WG_LANES_SPLIT": "0.3"},
+    "split60": {"WG_LANES_SPLIT": "0.6"},
     "sprio_hi": {"WG_LANES_PRIO": "-1"},
     "sprio_hi_L3": {"WG_LANES_PRIO": "-1", "WG_LANES": "3"},
     "prio0": {"WG_LEAN_PRIO": "0"},
@@ -35,7 +38,7 @@ VARIANTS = {
     "w2_L3": {"WG_LEAN_WAVES": "2", "WG_LANES": "3"},
     "w1_L4": {"WG_LEAN_WAVES": "1", "WG_LANES": "4"},
 }
-KEYS = ("WG_LEAN_PERSIST", "WG_LEAN_QUO", "WG_LEAN_WAVES", "WG_LEAN_PER_CU", "WG_LEAN_BLOCKS", "WG_LANES", "WG_LEAN_PRIO", "WG_LANES_PRIO")
+KEYS = ("WG_LEAN_PERSIST", "WG_LEAN_QUO", "WG_LEAN_WAVES", "WG_LEAN_PER_CU", "WG_LEAN_BLOCKS", "WG_LANES", "WG_LEAN_PRIO", "WG_LANES_PRIO", "WG_LANES_SPLIT")
 
 
 def main():

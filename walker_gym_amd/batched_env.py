@@ -238,7 +238,11 @@ class BatchedPhysicsEnv:
             nb = self.batch.plan_blocks
             bounds = [nb * i // lanes for i in range(lanes)] + [nb]
         else:
-            bounds = [0] + [((self.N * i // lanes) + 63) // 64 * 64 for i in range(1, lanes)] + [self.N]
+            f0 = float(os.environ.get("WG_LANES_SPLIT", "0"))   # experiments: first range's share (lanes 2)
+            if lanes == 2 and 0.0 < f0 < 1.0:
+                bounds = [0, min(self.N - 64, max(64, (int(self.N * f0) + 63) // 64 * 64)), self.N]
+            else:
+                bounds = [0] + [((self.N * i // lanes) + 63) // 64 * 64 for i in range(1, lanes)] + [self.N]
         done = []
         for i in range(lanes):
             w0, w1 = bounds[i], bounds[i + 1]

@@ -201,6 +201,37 @@ def test_size_extremes_vs_oracle(case):
     _oracle_compare(spec, dict(in3d=1), 8, acts)
 
 
+def _tiny_walkers(N, seed):
+    """Walkers of 1-3 masses: single free masses (no spring), pairs with one spring, triangles; some with no
+    muscle.  Exercises the smallest tiles of the workgroup kernel."""
+    rng = np.random.default_rng(seed)
+    m, pos, mo, ei, ej, rest, eo, nm = [], [], [0], [], [], [], [0], []
+    for w in range(N):
+        M = int(rng.integers(1, 4))
+        p = rng.uniform(-5, 5, (M, 3)).astype(np.float32)
+        p[:, 1] += 3.0
+        m += list(rng.uniform(0.5, 3, M)); pos += list(p); mo.append(mo[-1] + M)
+        pairs = [(0, 1)] if M == 2 else ([(0, 1), (1, 2), (0, 2)] if M == 3 else [])
+        for i, j in pairs:
+            ei.append(i); ej.append(j); rest.append(float(np.linalg.norm(p[i] - p[j])) * 0.9)
+        eo.append(len(ei))
+        nm.append(min(len(pairs), int(rng.integers(0, 2))))
+    E, U = len(ei), int(sum(nm))
+    P = len(m)
+    return dict(m=np.array(m, np.float32), pos=np.array(pos, np.float32), vel=np.zeros((P, 3), np.float32),
+                mass_off=np.array(mo, np.int32), ei=np.array(ei, np.int32), ej=np.array(ej, np.int32),
+                rest=np.array(rest, np.float32), k=np.full(E, 500.0, np.float32), c=np.full(E, 10.0, np.float32),
+                flags=(rng.random(E) < 0.3).astype(np.uint8), edge_off=np.array(eo, np.int32),
+                n_muscles=np.array(nm, np.int32), minl=np.full(U, 0.5, np.float32),
+                maxl=np.full(U, 1.5, np.float32), stride=np.full(U, 1.0, np.float32))
+
+
+def test_tiny_walkers_vs_oracle():
+    spec = _tiny_walkers(3000, seed=21)
+    acts = np.random.default_rng(21).uniform(-1, 1, (30, 3000, 1)).astype(np.float32)
+    _oracle_compare(spec, dict(in3d=1), 30, acts)
+
+
 def test_full_size_sampled_vs_oracle():
     """BASELINE config 3 size (65,536 canonical walkers): walkers are independent, so the oracle
     checks a sample of them (first, last and random walkers) after 10 full-batch GPU steps."""

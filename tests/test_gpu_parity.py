@@ -232,6 +232,35 @@ def test_tiny_walkers_vs_oracle():
     _oracle_compare(spec, dict(in3d=1), 30, acts)
 
 
+def _big_walkers(N, M, K, A, seed):
+    """N walkers of M masses and K random springs (the first A muscles)."""
+    from walker_gym_amd.synthetic import norm3_f32
+    rng = np.random.default_rng(seed)
+    pos = rng.uniform(-20, 20, (N * M, 3)).astype(np.float32)
+    pos[:, 1] += 25.0
+    ei = rng.integers(0, M, N * K).astype(np.int32)
+    ej = ((ei + rng.integers(1, M, N * K)) % M).astype(np.int32)
+    base = np.repeat(np.arange(N) * M, K)
+    rest = norm3_f32(pos[base + ei] - pos[base + ej]).astype(np.float32)
+    return dict(m=rng.uniform(1, 3, N * M).astype(np.float32), pos=pos, vel=np.zeros((N * M, 3), np.float32),
+                mass_off=(np.arange(N + 1) * M).astype(np.int32), ei=ei, ej=ej, rest=rest,
+                k=np.full(N * K, 200.0, np.float32), c=np.full(N * K, 5.0, np.float32),
+                flags=np.zeros(N * K, np.uint8), edge_off=(np.arange(N + 1) * K).astype(np.int32),
+                n_muscles=np.full(N, A, np.int32), minl=np.full(N * A, 0.5, np.float32),
+                maxl=np.full(N * A, 1.5, np.float32), stride=np.full(N * A, 1.0, np.float32))
+
+
+def test_largest_walkers():
+    """WG_MAX_M = 1024 masses: 1024-mass, 1024-spring walkers match the oracle on the workgroup kernel; walkers
+    whose spring terms cannot fit a workgroup's 160 KiB of LDS are refused before any launch (WG_ERANGE)."""
+    from walker_gym_amd.batched_env import BatchedPhysicsEnv
+    spec = _big_walkers(3, 1024, 1024, 8, seed=31)
+    acts = np.random.default_rng(31).uniform(-1, 1, (4, 3, 8)).astype(np.float32)
+    _oracle_compare(spec, dict(in3d=1), 4, acts)
+    with pytest.raises(ValueError, match="LDS"):
+        BatchedPhysicsEnv(_big_walkers(2, 1024, 6000, 0, seed=32), in3d=1).step(None)
+
+
 def test_full_size_sampled_vs_oracle():
     """BASELINE config 3 size (65,536 canonical walkers): walkers are independent, so the oracle
     checks a sample of them (first, last and random walkers) after 10 full-batch GPU steps."""

@@ -259,12 +259,27 @@ class BatchedPhysicsEnv:
                                  0 if T == 1 else self.N * cols, C.byref(o), n_steps, plan, nblk,
                                  C.c_void_p(st.cuda_stream)), "wg_step")
             if i:
-                actions.record_stream(st)   # the allocator must not recycle it before the side stream is done
+                if not torch.cuda.is_current_stream_capturing():
+                    actions.record_stream(st)   # the allocator must not recycle it before the side stream is done
                 ev = torch.cuda.Event()
                 ev.record(st)
                 done.append(ev)
         for ev in done:
             cur.wait_event(ev)
+
+    def graph(self, actions, n_steps: int, info: bool = True, lanes: Optional[int] = None):
+        """Capture run(actions, n_steps) into a HIP graph (torch.cuda.CUDAGraph over the ROCm runtime) and
+        return it; graph.replay() then advances the batch n_steps with one host call, the two walker ranges'
+        streams forked and joined inside the graph.  `actions` must stay alive (and may be refilled in place)
+        while the graph is used; the graph reads the batch and output tensors this env owns."""
+        g = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream(device=self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):           # capture off the default stream, as torch requires
+            with torch.cuda.graph(g, stream=side):
+                self.run(actions, n_steps, info=info, lanes=lanes)
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        return g
 
     def observe(self):
         o = self._outputs(self.obs, self.reward, self.done, self.centroid, self.energy)

@@ -261,6 +261,28 @@ def test_largest_walkers():
         BatchedPhysicsEnv(_big_walkers(2, 1024, 6000, 0, seed=32), in3d=1).step(None)
 
 
+def test_from_topologies_vs_oracle():
+    """BatchedPhysicsEnv.from_topologies: 4000 envs over Balance-v0 and Box-v0 vs the oracle."""
+    import torch
+    from oracle.oracle import Oracle
+    from walker_gym_amd.batched_env import BatchedPhysicsEnv
+    from walker_gym_amd.walker import (concat_specs, create_balance_creature, create_box_creature,
+                                       creatures_to_spec, replicate_spec)
+    env = BatchedPhysicsEnv.from_topologies(["Balance-v0", "Box-v0"], 4000, device="cuda:0", in3d=1)
+    spec = concat_specs([replicate_spec(creatures_to_spec([create_balance_creature()]), 2000),
+                         replicate_spec(creatures_to_spec([create_box_creature()]), 2000)])
+    orc = Oracle(spec, dict(in3d=1))
+    acts = np.random.default_rng(8).uniform(-1, 1, (20, 4000, 4)).astype(np.float32)
+    for t in range(20):
+        obs, rew, done, info = env.step(acts[t])
+        ref = orc.step(acts[t])
+    torch.cuda.synchronize()
+    _close(env.pos.cpu().numpy(), orc.pos)
+    _close(obs.cpu().numpy(), ref["obs"])
+    with pytest.raises(ValueError, match="Unknown environment ID"):
+        BatchedPhysicsEnv.from_topologies("Walker-v9", 8, device="cuda:0")
+
+
 def test_full_size_sampled_vs_oracle():
     """BASELINE config 3 size (65,536 canonical walkers): walkers are independent, so the oracle
     checks a sample of them (first, last and random walkers) after 10 full-batch GPU steps."""

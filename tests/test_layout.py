@@ -94,3 +94,15 @@ def test_pair_and_g3_host_plumbing():
     assert C.sizeof(s) > 0
     with pytest.raises(ValueError):
         EnvParams(g3_gravity=(0.0, 1.0)).to_struct()
+
+
+def test_concat_specs_matches_creatures_to_spec():
+    from walker_gym_amd.walker import concat_specs, create_box_creature, replicate_spec
+    a, b = create_balance_creature(), create_box_creature()
+    joined = concat_specs([replicate_spec(creatures_to_spec([a]), 3), replicate_spec(creatures_to_spec([b]), 2)])
+    ref = creatures_to_spec([a, a, a, b, b])
+    assert set(joined) == set(ref)
+    for k in ref:
+        assert np.array_equal(joined[k], ref[k]), k
+    h = pack(joined)
+    assert h.N == 5 and h.ragged   # Box-v0 has 4 muscles, Balance-v0 2: a ragged batch

@@ -100,6 +100,33 @@ class BatchedPhysicsEnv:
             self._gen.manual_seed(int(seed))
         self._alloc_outputs()
 
+    @classmethod
+    def from_topologies(cls, topologies, n_envs: int, device=None, **params) -> "BatchedPhysicsEnv":
+        """SURVEY §8(b)'s BatchedPhysicsEnv(topologies, n_envs, device, **EnvParams): n_envs walkers split into
+        contiguous, near-equal blocks, one per topology in order (uniform when there is one).  A topology is
+        a Creature (walker_gym_amd.walker / .topologies builders) or an env id of make_env ('Balance-v0',
+        'Box-v0', gym/optimized_env.py:273-294; unknown ids raise ValueError as there)."""
+        from .walker import (Creature, concat_specs, create_balance_creature, create_box_creature,
+                             creatures_to_spec, replicate_spec)
+        if isinstance(topologies, (str, Creature)):
+            topologies = [topologies]
+        topologies = list(topologies)
+        if not topologies or n_envs < len(topologies):
+            raise ValueError("need at least one topology and one env per topology")
+        specs = []
+        for t, topo in enumerate(topologies):
+            if isinstance(topo, str):
+                tid = topo.lower()
+                if tid == "balance-v0":
+                    topo = create_balance_creature()
+                elif tid == "box-v0":
+                    topo = create_box_creature()
+                else:
+                    raise ValueError(f"Unknown environment ID: {topo}")
+            count = n_envs // len(topologies) + (1 if t < n_envs % len(topologies) else 0)
+            specs.append(replicate_spec(creatures_to_spec([topo]), count))
+        return cls(specs[0] if len(specs) == 1 else concat_specs(specs), device=device, **params)
+
     # ------------------------------------------------------------------ plumbing
     def _alloc_outputs(self):
         N, D, dv = self.N, self.obs_dim, self.device

@@ -150,6 +150,27 @@ def replicate_spec(spec: dict, n: int) -> dict:
     return out
 
 
+def concat_specs(specs: List[dict]) -> dict:
+    """Walkers of several flat CSR specs, in order, as one spec (offsets rebased)."""
+    out = {}
+    per = ("m", "pos", "vel", "acc", "ei", "ej", "rest", "k", "c", "flags", "minl", "maxl", "stride", "mx",
+           "pinned", "charge", "radius", "n_muscles")
+    for key in per:
+        parts = [np.asarray(s[key]) for s in specs if key in s]
+        if len(parts) == len(specs):
+            out[key] = np.concatenate(parts)
+        elif parts:
+            raise ValueError(f"concat_specs: '{key}' present in some specs only")
+    for key in ("mass_off", "edge_off"):
+        offs, base = [np.zeros(1, np.int32)], 0
+        for s in specs:
+            o = np.asarray(s[key], np.int64)
+            offs.append((o[1:] + base).astype(np.int32))
+            base += int(o[-1])
+        out[key] = np.concatenate(offs)
+    return out
+
+
 def balance_spec(n: int = 1) -> dict:
     return replicate_spec(creatures_to_spec([create_balance_creature()]), n)
 

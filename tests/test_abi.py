@@ -81,6 +81,7 @@ def test_errors_without_gpu(lib):
     assert lib.wg_step(C.byref(b), C.byref(p), None, 0, 0, 0, None, 1, None, 0, None) == _lib.WG_ERANGE
     with pytest.raises(ValueError):
         _lib.check(-1, "probe")
+    assert lib.wg_reset_noise(None, None, None) == _lib.WG_EINVAL
     # pair gravity runs on the wave-per-walker-group kernel only: a ragged batch is refused before any launch
     b = _lib.WgBatch(N=4, M=8, K=4, A=0, ragged=1)
     for f in ("pos", "vel", "acc", "mass", "edges", "inc", "inc_off", "muscle_x", "steps", "mass_off", "edge_off",

@@ -283,6 +283,31 @@ def test_from_topologies_vs_oracle():
         BatchedPhysicsEnv.from_topologies("Walker-v9", 8, device="cuda:0")
 
 
+def test_reset_noise_entry_point():
+    """wg_reset_noise == PhysicsEnv.reset with all three noise components (wg_reset, in3d)."""
+    import ctypes as C
+
+    import torch
+    from walker_gym_amd import _lib
+    from walker_gym_amd.batched_env import BatchedPhysicsEnv
+    from walker_gym_amd.synthetic import canonical_walkers
+    N = 2048
+    env = BatchedPhysicsEnv(canonical_walkers(N, seed=17), device="cuda:0", in3d=1)
+    acts = np.random.default_rng(17).uniform(-1, 1, (5, N, 8)).astype(np.float32)
+    for t in range(5):
+        env.step(acts[t])
+    sd = env.batch.state_dict()
+    noise = torch.randn((N * 16, 3), generator=torch.Generator(device="cuda:0").manual_seed(17), device="cuda:0")
+    env.reset(noise)
+    torch.cuda.synchronize()
+    ref = [t.clone() for t in env.batch.state_dict().values()]
+    env.batch.load_state_dict(sd)
+    _lib.check(_lib.load().wg_reset_noise(C.byref(env.batch.struct), C.c_void_p(noise.data_ptr()),
+                                          C.c_void_p(torch.cuda.current_stream().cuda_stream)), "wg_reset_noise")
+    torch.cuda.synchronize()
+    assert all(torch.equal(a, b) for a, b in zip(ref, env.batch.state_dict().values()))
+
+
 def test_full_size_sampled_vs_oracle():
     """BASELINE config 3 size (65,536 canonical walkers): walkers are independent, so the oracle
     checks a sample of them (first, last and random walkers) after 10 full-batch GPU steps."""

@@ -53,8 +53,8 @@ class WgLaunchInfo(C.Structure):
                 ("lds_bytes", C.c_int32)]
 
 
-EXPORTS = ("wg_abi_version", "wg_last_error", "wg_step", "wg_observe", "wg_reset", "wg_plan_ragged",
-           "wg_launch_geometry")
+EXPORTS = ("wg_abi_version", "wg_last_error", "wg_step", "wg_observe", "wg_reset", "wg_reset_noise",
+           "wg_plan_ragged", "wg_launch_geometry")
 
 _lib = None
 _lock = threading.Lock()
@@ -82,9 +82,10 @@ def load(path: str | None = None):
                               C.POINTER(WgOutputs), C.c_int32, _vp, C.c_int32, _vp]
         L.wg_observe.argtypes = [C.POINTER(WgBatch), C.POINTER(WgParams), C.POINTER(WgOutputs), _vp, C.c_int32, _vp]
         L.wg_reset.argtypes = [C.POINTER(WgBatch), C.POINTER(WgParams), _vp, _vp, _vp]
+        L.wg_reset_noise.argtypes = [C.POINTER(WgBatch), _vp, _vp]
         L.wg_plan_ragged.argtypes = [_vp, _vp, _vp, C.c_int32, _vp, C.c_int32]
         L.wg_launch_geometry.argtypes = [C.POINTER(WgBatch), C.POINTER(WgLaunchInfo)]
-        for f in ("wg_step", "wg_observe", "wg_reset", "wg_plan_ragged", "wg_launch_geometry"):
+        for f in ("wg_step", "wg_observe", "wg_reset", "wg_reset_noise", "wg_plan_ragged", "wg_launch_geometry"):
             getattr(L, f).restype = C.c_int
         v = L.wg_abi_version()
         if v != ABI_VERSION:

@@ -2154,6 +2154,12 @@ int wg_reset(const wg_batch *b, const wg_params *p, const float *noise, const ui
     return 0;
 }
 
+int wg_reset_noise(const wg_batch *b, const float *noise, hipStream_t stream) {
+    wg_params p{};
+    p.in3d = 1;   // every component of noise is added: a 2D caller passes z = 0 (v.z + 0 == v.z)
+    return wg_reset(b, &p, noise, nullptr, stream);
+}
+
 int wg_plan_ragged(const int32_t *mass_off, const int32_t *edge_off, const int32_t *muscle_off,
                    int32_t N, int32_t *plan, int32_t max_blocks) {
     if (!mass_off || !edge_off || !muscle_off || !plan || N < 0 || max_blocks < 1)

@@ -107,10 +107,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("WG_DIST_BACKEND", "nccl")   # nccl = RCCL; gloo only to rehearse ranks on one GPU
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -139,7 +145,10 @@ def main():
     env.run(acts, args.steps)
     ev1.record(stream)
     if world > 1 and not args.no_gather:
-        dist.all_gather_into_tensor(gather_buf, env.obs)      # rollout-end observation gather (RCCL)
+        if backend == "nccl":
+            dist.all_gather_into_tensor(gather_buf, env.obs)  # rollout-end observation gather (RCCL)
+        else:
+            dist.all_gather(list(gather_buf.chunk(world, 0)), env.obs)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

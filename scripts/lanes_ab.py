@@ -11,8 +11,9 @@ from bench import make_spec  # noqa: E402
 from walker_gym_amd.batched_env import BatchedPhysicsEnv  # noqa: E402
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+WORKLOAD = sys.argv[2] if len(sys.argv) > 2 else "canonical"
 STEPS = 500
-spec, params = make_spec("canonical", N, seed=1000)
+spec, params = make_spec(WORKLOAD, N, seed=1000)
 env = BatchedPhysicsEnv(spec, device="cuda:0", **params)
 gen = torch.Generator(device="cuda:0")
 gen.manual_seed(7)

@@ -446,13 +446,13 @@ def test_graph_replay_equals_run():
     acts = (torch.rand((10, N, 8), generator=torch.Generator(device="cuda:0").manual_seed(6), device="cuda:0")
             * 2 - 1).contiguous()
     sd0 = env.batch.state_dict()
-    env.run(acts, 10)
-    env.run(acts, 10)
+    env.run(acts, 10, lanes=1)
+    env.run(acts, 10, lanes=1)
     torch.cuda.synchronize()
     ref = [t.clone() for t in env.batch.state_dict().values()] + [env.obs.clone(), env.energy.clone()]
     env.batch.load_state_dict(sd0)
     torch.cuda.synchronize()
-    g = env.graph(acts, 10)          # capture records the launches without running them
+    g = env.graph(acts, 10, lanes=2)   # capture records the launches (two streams) without running them
     env.batch.load_state_dict(sd0)
     torch.cuda.synchronize()
     g.replay()

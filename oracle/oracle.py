@@ -29,7 +29,7 @@ class OrcParams(C.Structure):
                [(n, C.c_double) for n in ("pair_g", "pair_k", "pair_e", "bounce_k")] + \
                [("g3_gravity", C.c_double * 3)] + \
                [(n, C.c_double) for n in ("g3_damping", "g3_air", "g3_ground_level", "g3_restitution",
-                                          "g3_friction")] + [("g3_ground", C.c_int32)]
+                                          "g3_friction")] + [("g3_ground", C.c_int32), ("friction_mode", C.c_int32)]
 
 
 class OrcBatch(C.Structure):
@@ -81,7 +81,7 @@ DEFAULT_PARAMS = dict(g=100.0, dampk=0.0, ground=0.0, groundk=1000.0, grounddamp
                       conmid=0, spring_mode=0, action_mode=0, integrator=1, pair_mode=0, pair_g=9.8,
                       pair_k=8.99e9, pair_e=16e-20, bounce_k=100.0,
                       g3_gravity=(0.0, -9.8, 0.0), g3_damping=0.99, g3_air=0.01, g3_ground_level=-50.0,
-                      g3_restitution=0.8, g3_friction=0.5, g3_ground=1)
+                      g3_restitution=0.8, g3_friction=0.5, g3_ground=1, friction_mode=0)
 
 
 class Oracle:

@@ -26,7 +26,7 @@
 #include <omp.h>
 #endif
 
-#define ORC_ABI 3
+#define ORC_ABI 4
 int orc_abi_version(void) { return ORC_ABI; }
 
 /* Config.r (gym/engine.py:9, gym/optimized_engine.py:7): the distance clamp, a Python float. */
@@ -304,8 +304,11 @@ static void walker_step(const orc_batch *b, const orc_params *p, int w, const fl
             a[0] = add_f32(a[0], 0.f, mf); a[1] = add_f32(a[1], gk * deep, mf); a[2] = add_f32(a[2], 0.f, mf);
             a[0] = add_f32(a[0], 0.f, mf); a[1] = add_f32(a[1], gd * v[1], mf); a[2] = add_f32(a[2], 0.f, mf);
             const float ff = fabsf(deep) * fr;
-            a[0] = add_f32(a[0], (-v[0]) * ff, mf); a[1] = add_f32(a[1], 0.f, mf);
-            a[2] = add_f32(a[2], (-v[2]) * ff, mf);
+            /* friction_mode 1: the G1 env's [v_x*deep*friction, 0, v_z*deep*friction] (gym/env.py:41) */
+            const float fx = p->friction_mode ? (v[0] * deep) * fr : (-v[0]) * ff;
+            const float fz = p->friction_mode ? (v[2] * deep) * fr : (-v[2]) * ff;
+            a[0] = add_f32(a[0], fx, mf); a[1] = add_f32(a[1], 0.f, mf);
+            a[2] = add_f32(a[2], fz, mf);
         }
         if (b->contact) b->contact[q] = (uint8_t)hit;   /* replaces color/r (optimized_env.py:155-175) */
         if (b->radius) b->radius[q] = hit ? 3.0 : 1.0;  /* p.r = 3 / p.r = 1 (optimized_env.py:156,175) */

@@ -31,6 +31,8 @@ typedef struct orc_params {
     double g3_gravity[3];  /* Environment.gravity (default (0, -9.8, 0)) */
     double g3_damping, g3_air, g3_ground_level, g3_restitution, g3_friction;
     int32_t g3_ground;     /* Environment.ground: the position-clamp ground is on */
+    int32_t friction_mode; /* ground friction: 0 = [-v_x*(|deep|*friction), 0, -v_z*(...)] (gym/optimized_env.py:
+                              168-172); 1 = [v_x*deep*friction, 0, v_z*deep*friction] (the G1 env, gym/env.py:41) */
 } orc_params;
 
 typedef struct orc_batch {

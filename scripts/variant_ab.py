@@ -1,0 +1,85 @@
+#!/usr/bin/env python3
+"""Compile-time A/B of the step kernel (profiling aid, not product).
+
+    python scripts/variant_ab.py build NAME=FLAGS ...     # here (CPU): build_ab/lib_NAME.so, e.g.
+                                                          #   base= soa0=-DWG_LEAN_SOA=0 abl1=-DWG_ABLATE=1
+    python scripts/variant_ab.py run [rounds] [workload]  # GPU box: every .so in build_ab/, interleaved rounds
+
+Each (variant, round) runs in its own process (WALKER_HIP_LIB picks the library) on the bench workload and
+reports the per-launch time with HIP events for one full-batch launch per step (lanes 1) and for bench.py's
+default walker ranges (lanes 2); the summary is the median over rounds.  Results are written to
+gpurun_out/variant_ab.json."""
+import json
+import os
+import statistics
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+OUT = os.path.join(ROOT, "build_ab")
+
+
+def build(specs):
+    from walker_gym_amd import build as wb
+    os.makedirs(OUT, exist_ok=True)
+    jobs = []
+    for spec in specs:
+        name, _, flags = spec.partition("=")
+        cmd = wb.command(os.path.join(OUT, f"lib_{name}.so"))
+        cmd = cmd[:-1] + flags.split() + cmd[-1:]
+        jobs.append((name, subprocess.Popen(cmd)))
+    for name, j in jobs:
+        assert j.wait() == 0, name
+        print("built", name)
+
+
+def time_one(lib, workload, steps=200, warm=20):
+    os.environ["WALKER_HIP_LIB"] = lib
+    import torch
+    from bench import make_spec
+    from walker_gym_amd.batched_env import BatchedPhysicsEnv
+    n = int(os.environ.get("WG_N", "65536"))
+    spec, params = make_spec(workload, n, seed=1000)
+    env = BatchedPhysicsEnv(spec, device="cuda:0", **params)
+    acts = (torch.rand((steps, n, env.batch.A), device="cuda:0") * 2 - 1).contiguous()
+    res = {}
+    for lanes in (1, 2):
+        env.run(acts[:warm].contiguous(), warm, lanes=lanes)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        env.run(acts, steps, lanes=lanes)
+        e1.record()
+        torch.cuda.synchronize()
+        res[f"lanes{lanes}"] = e0.elapsed_time(e1) / steps * 1e3
+    return res
+
+
+def run(rounds, workload):
+    libs = sorted(f for f in os.listdir(OUT) if f.endswith(".so"))
+    allr = {f[4:-3]: [] for f in libs}
+    for r in range(rounds):
+        for f in libs:
+            p = subprocess.run([sys.executable, __file__, "one", os.path.join(OUT, f), workload], capture_output=True,
+                               text=True, timeout=300)
+            if p.returncode:
+                print(f, "FAILED", p.stderr[-400:], flush=True)
+                raise SystemExit(1)
+            allr[f[4:-3]].append(json.loads(p.stdout.strip().splitlines()[-1]))
+            print(r, f, p.stdout.strip().splitlines()[-1], flush=True)
+    summ = {k: {m: round(statistics.median(x[m] for x in v), 2) for m in v[0]} for k, v in allr.items()}
+    for k, v in summ.items():
+        print(f"{k:16s} " + "  ".join(f"{m} {x:7.2f} us" for m, x in v.items()))
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    json.dump({"workload": workload, "rounds": rounds, "median_us_per_step": summ, "all": allr},
+              open(os.path.join(ROOT, "gpurun_out", f"variant_ab_{workload}.json"), "w"), indent=1)
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "build":
+        build(sys.argv[2:])
+    elif sys.argv[1] == "run":
+        run(int(sys.argv[2]) if len(sys.argv) > 2 else 5, sys.argv[3] if len(sys.argv) > 3 else "canonical")
+    else:
+        print(json.dumps(time_one(sys.argv[2], sys.argv[3])))

@@ -82,15 +82,25 @@ def test_errors_without_gpu(lib):
     with pytest.raises(ValueError):
         _lib.check(-1, "probe")
     assert lib.wg_reset_noise(None, None, None) == _lib.WG_EINVAL
-    # pair gravity runs on the wave-per-walker-group kernel only: a ragged batch is refused before any launch
+    # pair passes need the engine.py spring (spring_mode 0): refused before any launch
     b = _lib.WgBatch(N=4, M=8, K=4, A=0, ragged=1)
     for f in ("pos", "vel", "acc", "mass", "edges", "inc", "inc_off", "muscle_x", "steps", "mass_off", "edge_off",
               "muscle_off"):
         setattr(b, f, 16)
-    p = _lib.WgParams(pair_mode=1, pair_g=9.8)
+    p = _lib.WgParams(pair_mode=1, pair_g=9.8, spring_mode=1)
     plan = np.zeros(2, np.int32)
     assert lib.wg_step(C.byref(b), C.byref(p), None, 0, 0, 0, None, 1, plan.ctypes.data_as(C.c_void_p), 1, None) == _lib.WG_EINVAL
     assert b"pair_mode" in lib.wg_last_error()
+    # ragged kinds: 0, 1 (workgroup plan), 2 (wave plan, M <= 64 only); a walker permutation only for ragged batches
+    p = _lib.WgParams()
+    for kind, M in ((3, 8), (2, 65)):
+        b.ragged, b.M = kind, M
+        assert lib.wg_step(C.byref(b), C.byref(p), None, 0, 0, 0, None, 1, plan.ctypes.data_as(C.c_void_p), 1,
+                           None) == _lib.WG_EINVAL
+    b.ragged, b.M, b.row = 0, 8, 16
+    assert lib.wg_step(C.byref(b), C.byref(p), None, 0, 0, 0, None, 1, None, 0, None) == _lib.WG_EINVAL
+    assert b"row" in lib.wg_last_error()
+    b.row = None
     # unknown pair bits, and bounce without the radius array, are refused before any launch
     b.ragged = 0
     for pm in (8, 4):

@@ -1,10 +1,13 @@
-"""World-size-2 gloo test of the sharded path: each rank steps its contiguous walker
-shard (here with the CPU oracle standing in for the GPU kernel — the plumbing under test is the shard
-split and the rollout-end gather), gathers observations, and the result equals the unsharded batch."""
+"""World-size-2/3 gloo tests of the sharded path on the CPU: each rank steps its contiguous
+walker shard (here with the CPU oracle standing in for the GPU kernel — the plumbing under test is the shard
+split and the rollout-end gather, including uneven shards), gathers observations, and the result equals the
+unsharded batch.  The same path through the HIP kernel is test_gpu_distributed.py; bench.py's own rank
+launcher is test_bench_launcher.py."""
 import os
 import socket
 
 import numpy as np
+import pytest
 import torch.multiprocessing as mp
 
 from walker_gym_amd.distributed import shard_bounds, shard_spec
@@ -18,7 +21,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n_total, T, out_q):
+def _worker(rank, world, port, n_total, T, out_q, by_size):
     import torch
     import torch.distributed as dist
     from oracle.oracle import Oracle
@@ -34,7 +37,7 @@ def _worker(rank, world, port, n_total, T, out_q):
     obs = None
     for t in range(T):
         obs = orc.step(acts[t, a:b])["obs"]
-    full = gather_rollout(torch.from_numpy(obs))
+    full = gather_rollout(torch.from_numpy(obs), n_total=None if by_size else n_total)
     if rank == 0:
         out_q.put(full.numpy())
     dist.barrier()
@@ -50,14 +53,16 @@ def test_shard_bounds_cover():
             assert max(b - a for a, b in rs) - min(b - a for a, b in rs) <= 1
 
 
-def test_gloo_world2_matches_single_process():
+@pytest.mark.parametrize("world,n_total,by_size", [(2, 64, False), (2, 65, False), (3, 65, True)])
+def test_gloo_matches_single_process(world, n_total, by_size):
+    """Even and uneven shards (65 walkers: ranks of 33/32 or 22/22/21), lengths from shard_bounds or gathered."""
     from oracle.oracle import Oracle
     from walker_gym_amd.synthetic import canonical_walkers
-    n_total, T = 64, 5
+    T = 5
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, n_total, T, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_total, T, q, by_size)) for r in range(world)]
     for p in procs:
         p.start()
     got = q.get(timeout=180)
@@ -69,4 +74,5 @@ def test_gloo_world2_matches_single_process():
     orc = Oracle(spec, dict(in3d=1))
     for t in range(T):
         ref = orc.step(acts[t])["obs"]
+    assert got.shape == ref.shape
     assert np.array_equal(got, ref)

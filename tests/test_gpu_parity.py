@@ -460,33 +460,71 @@ def test_graph_replay_equals_run():
     torch.cuda.synchronize()
     got = [t.clone() for t in env.batch.state_dict().values()] + [env.obs.clone(), env.energy.clone()]
     assert all(torch.equal(a, b) for a, b in zip(ref, got))
+    # the graph holds the parameters and buffers as captured: after set_params it refuses to replay
+    env.set_params(dampk=0.5)
+    with pytest.raises(RuntimeError, match="stale"):
+        g.replay()
 
 
-def test_kernel_variants_agree(tmp_path):
-    """The wave-independent lean kernel (default for uniform M | 64 batches), the workgroup kernel it
-    replaced (WG_LEAN=0) and the lean variants (prefetching persistent waves, end quotients formed in the
-    edge phase) restate the same arithmetic: their outputs must be bitwise equal, including a batch whose
-    last wave is only partly filled."""
-    import subprocess
-    import sys
-    here = os.path.dirname(os.path.abspath(__file__))
-    outs = {}
-    variants = (("lean", {}), ("barrier", {"WG_LEAN": "0"}),
-                # persistent waves with next-tile prefetch; a small grid so every wave walks many tiles
-                ("prefetch", {"WG_LEAN_PERSIST": "2", "WG_LEAN_BLOCKS": "3"}),
-                # end quotients formed in the edge phase, one tile per wave and persistent + prefetch
-                ("quo", {"WG_LEAN_QUO": "1"}),
-                ("quo_prefetch", {"WG_LEAN_QUO": "1", "WG_LEAN_PERSIST": "2", "WG_LEAN_BLOCKS": "5"}))
-    for tag, env in variants:
-        path = str(tmp_path / f"{tag}.npz")
-        subprocess.run([sys.executable, os.path.join(here, "kernel_variant_run.py"), path],
-                       env=dict(os.environ, **env), check=True, timeout=300)
-        outs[tag] = np.load(path)
-    a = outs["lean"]
-    for tag, _ in variants[1:]:
-        b = outs[tag]
-        assert sorted(a.files) == sorted(b.files), tag
-        for k in a.files:
-            x, y = a[k], b[k]
-            assert x.shape == y.shape, (tag, k)
-            assert np.array_equal(x.view(np.uint8), y.view(np.uint8)), (tag, k)
+def test_run_and_rollout_refuse_foreign_tensors():
+    """run()/rollout() hand raw pointers to the kernel: host tensors, other dtypes and non-contiguous outputs are
+    refused before any launch."""
+    import torch
+    from walker_gym_amd.batched_env import BatchedPhysicsEnv
+    from walker_gym_amd.synthetic import canonical_walkers
+    env = BatchedPhysicsEnv(canonical_walkers(64, seed=1), device="cuda:0", in3d=1)
+    good = torch.zeros((2, 64, 8), device="cuda:0")
+    for bad in (torch.zeros((2, 64, 8)), torch.zeros((2, 64, 8), device="cuda:0", dtype=torch.float64),
+                torch.zeros((2, 8, 64), device="cuda:0").transpose(1, 2)):
+        with pytest.raises(ValueError):
+            env.run(bad, 2)
+    env.run(good, 2)
+    with pytest.raises(ValueError):
+        env.rollout(good, obs_out=torch.zeros((2, 64, env.obs_dim)))
+    with pytest.raises(ValueError):
+        env.rollout(good, done_out=torch.zeros((2, 64), device="cuda:0"))
+    with pytest.raises(ValueError):
+        env.rollout(good, reward_out=torch.zeros((64, 2), device="cuda:0").t())
+
+
+def _variant_cases():
+    from walker_gym_amd.synthetic import canonical_walkers
+    from walker_gym_amd.topologies import topology_spec
+    from walker_gym_amd.walker import balance_spec
+    pinned = canonical_walkers(700, seed=13)
+    pinned["pinned"] = (np.random.default_rng(13).random(700 * 16) < 0.1).astype(np.uint8)
+    pinned["vel"] = np.random.default_rng(14).normal(0, 1, (700 * 16, 3)).astype(np.float32)
+    return [("canonical", canonical_walkers(1003, seed=11), dict(in3d=1), 8),   # 1003: a partial last wave
+            ("balance", balance_spec(997), dict(in3d=0), 2),
+            ("canonical2d", canonical_walkers(640, seed=12), dict(in3d=0, dampk=0.2, midform=0), 8),
+            ("pinned_run2", pinned, dict(in3d=1, integrator=2), 8),
+            ("g1_box2", topology_spec("box2", 997, 1), dict(in3d=0, midform=2, conmid=1), 4)]
+
+
+def _variant_run(spec, params, A, name):
+    import torch
+    from walker_gym_amd.batched_env import BatchedPhysicsEnv
+    N = len(spec["mass_off"]) - 1
+    acts = np.random.default_rng(len(name)).uniform(-1, 1, (25, N, A)).astype(np.float32)
+    env = BatchedPhysicsEnv(spec, device="cuda", **params)
+    o, r, d = env.rollout(acts)
+    torch.cuda.synchronize()
+    out = [o, r, d] + [getattr(env, f)
+                       for f in ("pos", "vel", "acc", "muscle_x", "contact", "steps")]
+    return [t.cpu().numpy() for t in out]
+
+
+def test_kernel_variants_agree():
+    """The wave-independent lean kernel (default for uniform M | 64 batches) and the workgroup kernel
+    (WG_LEAN=0, read by libwalker_hip.so on every call) restate the same arithmetic: their outputs must be
+    bitwise equal, including a batch whose last wave is only partly filled."""
+    for name, spec, params, A in _variant_cases():
+        lean = _variant_run(spec, params, A, name)
+        os.environ["WG_LEAN"] = "0"
+        try:
+            wg = _variant_run(spec, params, A, name)
+        finally:
+            del os.environ["WG_LEAN"]
+        for x, y in zip(lean, wg):
+            assert x.shape == y.shape, name
+            assert np.array_equal(x.view(np.uint8), y.view(np.uint8)), name

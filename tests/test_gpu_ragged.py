@@ -1,0 +1,174 @@
+"""Ragged batches on the GPU, through the C ABI:
+
+* the wave kernel (wg_batch.ragged = 2: walkers sorted by size, packed into wave tiles by wg_plan_waves) is
+  bitwise equal to the workgroup kernel running the same plan (WG_LEAN=0), and both to the oracle with the
+  outputs back in the caller's walker order;
+* pair forces (gym/engine.py:114-147 per walker) on the workgroup kernel: ragged batches and uniform walkers
+  whose M does not divide 64 match the oracle bit for bit;
+* reset noise and masks given in the caller's order land on the right (sorted) walkers; wg_reset_noise keeps a
+  2D walker's v.z = -0.0.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+from conftest import gpu_available
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not gpu_available():
+        pytest.skip("no ROCm GPU")
+
+
+def _rollout(spec, params, acts, lean=True):
+    import torch
+    from walker_gym_amd.batched_env import BatchedPhysicsEnv
+    if not lean:
+        os.environ["WG_LEAN"] = "0"
+    try:
+        env = BatchedPhysicsEnv(spec, device="cuda:0", **params)
+        o, r, d = env.rollout(acts)
+        torch.cuda.synchronize()
+        out = [o, r, d, env.pos, env.vel, env.acc, env.muscle_x, env.contact, env.steps, env.centroid, env.energy]
+        return env, [t.cpu().numpy() for t in out]
+    finally:
+        os.environ.pop("WG_LEAN", None)
+
+
+@pytest.mark.parametrize("params", [dict(in3d=1, dampk=0.3), dict(in3d=0, midform=2, conmid=1),
+                                    dict(in3d=1, integrator=2, midform=0)])
+def test_wave_kernel_equals_workgroup_kernel(params):
+    from walker_gym_amd.synthetic import ragged_walkers
+    N = 3001
+    spec = ragged_walkers(N, seed=41, mmin=2, mmax=48, string_frac=0.1)
+    A = int(np.max(spec["n_muscles"]))
+    acts = np.random.default_rng(41).uniform(-1, 1, (12, N, A)).astype(np.float32)
+    env, wave = _rollout(spec, params, acts, lean=True)
+    assert env.batch.ragged_kind == 2 and env.batch.row is not None
+    _, wg = _rollout(spec, params, acts, lean=False)
+    for x, y in zip(wave, wg):
+        assert np.array_equal(x.view(np.uint8), y.view(np.uint8))
+
+
+def test_wave_kernel_vs_oracle_caller_order():
+    """63 walkers of descending size (the sort reverses them); one walker of M = 64 fills a wave alone."""
+    import torch
+    from oracle.oracle import Oracle
+    from walker_gym_amd.batched_env import BatchedPhysicsEnv
+    from walker_gym_amd.synthetic import ragged_walkers
+    parts = [ragged_walkers(1, seed=100 + i, mmin=m, mmax=m) for i, m in enumerate(range(64, 1, -1))]
+    from walker_gym_amd.walker import concat_specs
+    spec = concat_specs(parts)
+    N = len(spec["mass_off"]) - 1
+    A = int(np.max(spec["n_muscles"]))
+    acts = np.random.default_rng(5).uniform(-1, 1, (15, N, A)).astype(np.float32)
+    env = BatchedPhysicsEnv(spec, device="cuda:0", in3d=1)
+    assert env.batch.ragged_kind == 2
+    orc = Oracle(spec, dict(in3d=1))
+    for t in range(15):
+        obs, rew, done, info = env.step(acts[t])
+        ref = orc.step(acts[t])
+    torch.cuda.synchronize()
+    assert np.array_equal(env.pos.cpu().numpy(), orc.pos)
+    assert np.array_equal(obs.cpu().numpy(), ref["obs"])
+    assert np.array_equal(rew.cpu().numpy(), ref["reward"])
+    assert np.array_equal(info["centroid_position"].cpu().numpy(), ref["centroid"])
+    assert np.array_equal(env.muscle_x.cpu().numpy(), orc.mx)
+
+
+@pytest.mark.parametrize("case", ["ragged", "uniform_M13", "uniform_M100"])
+def test_pair_forces_workgroup_kernel_vs_oracle(case):
+    import torch
+    from oracle.oracle import Oracle
+    from walker_gym_amd.batched_env import BatchedPhysicsEnv
+    from walker_gym_amd.synthetic import canonical_walkers, ragged_walkers
+    from walker_gym_amd.topologies import topology_spec
+    rng = np.random.default_rng(7)
+    if case == "ragged":
+        spec = ragged_walkers(600, seed=7, mmin=3, mmax=40)
+    elif case == "uniform_M13":
+        spec = topology_spec("insect", 500, 1)
+    else:
+        spec = canonical_walkers(40, seed=7, M=100, K=180, A=10)
+    P = int(spec["mass_off"][-1])
+    spec["charge"] = rng.uniform(-3, 3, P)
+    spec["radius"] = rng.uniform(0.5, 2.0, P)
+    N = len(spec["mass_off"]) - 1
+    A = max(1, int(np.max(spec["n_muscles"])))
+    params = dict(in3d=1, pair_mode=7, pair_g=500.0, pair_k=2.0e3, bounce_k=400.0)
+    env = BatchedPhysicsEnv(spec, device="cuda:0", **params)
+    orc = Oracle(spec, params)
+    acts = rng.uniform(-1, 1, (10, N, A)).astype(np.float32)
+    for t in range(10):
+        obs, rew, done, info = env.step(acts[t])
+        ref = orc.step(acts[t])
+    torch.cuda.synchronize()
+    assert np.array_equal(env.pos.cpu().numpy(), orc.pos, equal_nan=True)
+    assert np.array_equal(env.vel.cpu().numpy(), orc.vel, equal_nan=True)
+    assert np.array_equal(obs.cpu().numpy(), ref["obs"], equal_nan=True)
+    assert np.array_equal(env.batch.caller("radius").cpu().numpy(), orc.radius)
+
+
+def test_ragged_reset_noise_and_mask_in_caller_order():
+    import torch
+    from oracle.oracle import Oracle
+    from walker_gym_amd.batched_env import BatchedPhysicsEnv
+    from walker_gym_amd.synthetic import ragged_walkers
+    N = 500
+    spec = ragged_walkers(N, seed=9, mmin=2, mmax=30)
+    P = int(spec["mass_off"][-1])
+    env = BatchedPhysicsEnv(spec, device="cuda:0", in3d=1)
+    assert env.batch.row is not None
+    noise = np.random.default_rng(9).normal(0, 0.5, (P, 3)).astype(np.float32)
+    orc = Oracle(spec, dict(in3d=1))
+    env.reset(noise)
+    orc.reset(noise)
+    torch.cuda.synchronize()
+    assert np.array_equal(env.vel.cpu().numpy(), orc.vel)
+    # masked reset: only odd caller walkers
+    A = int(np.max(spec["n_muscles"]))
+    acts = np.random.default_rng(10).uniform(-1, 1, (3, N, A)).astype(np.float32)
+    for t in range(3):
+        env.step(acts[t])
+    mask = (np.arange(N) % 2).astype(np.uint8)
+    v_before = env.vel.cpu().numpy()
+    env.reset(noise, mask=mask)
+    torch.cuda.synchronize()
+    v_after = env.vel.cpu().numpy()
+    steps = env.steps.cpu().numpy()
+    wid = np.repeat(np.arange(N), np.diff(spec["mass_off"]))
+    sel = mask[wid] == 1
+    assert np.array_equal(v_after[~sel], v_before[~sel])
+    assert np.array_equal(v_after[sel], (v_before + noise)[sel])
+    assert np.array_equal(steps, np.where(mask == 1, 0, 3))
+
+
+def test_reset_noise_2d_keeps_negative_zero():
+    """wg_reset_noise skips noise components that are exactly +0.0: a 2D caller's z = +0.0 leaves v.z = -0.0 as it
+    is, bit for bit the same as wg_reset with in3d = 0 (PhysicsEnv.reset adds x and y only in 2D)."""
+    import torch
+    from walker_gym_amd import _lib
+    from walker_gym_amd.batched_env import BatchedPhysicsEnv
+    from walker_gym_amd.walker import balance_spec
+    spec = balance_spec(256)
+    spec["vel"] = np.zeros_like(spec["vel"])
+    spec["vel"][:, 2] = -0.0
+    env = BatchedPhysicsEnv(spec, device="cuda:0", in3d=0)
+    noise = torch.randn((256 * 4, 3), generator=torch.Generator(device="cuda:0").manual_seed(3), device="cuda:0")
+    noise[:, 2] = 0.0
+    sd = env.batch.state_dict()
+    env.reset(noise)                          # wg_reset, in3d = 0: x, y only
+    torch.cuda.synchronize()
+    ref = env.vel.clone()
+    env.batch.load_state_dict(sd)
+    _lib.check(_lib.load().wg_reset_noise(C.byref(env.batch.struct), C.c_void_p(noise.data_ptr()),
+                                          C.c_void_p(torch.cuda.current_stream().cuda_stream)), "wg_reset_noise")
+    torch.cuda.synchronize()
+    got = env.vel
+    assert torch.equal(got.view(torch.int32), ref.view(torch.int32))
+    assert (got[:, 2].view(torch.int32) == np.int32(-2 ** 31)).all()   # still -0.0

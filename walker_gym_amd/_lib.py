@@ -13,7 +13,7 @@ import threading
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libwalker_hip.so"
 LIB_PATH = os.path.join(HERE, LIB_NAME)
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 WG_EINVAL, WG_ERANGE, WG_EHIP = -1, -2, -3
 
@@ -28,7 +28,7 @@ class WgParams(C.Structure):
                [(n, C.c_double) for n in ("pair_g", "pair_k", "pair_e", "bounce_k")] + \
                [("g3_gravity", C.c_double * 3)] + \
                [(n, C.c_double) for n in ("g3_damping", "g3_air", "g3_ground_level", "g3_restitution",
-                                          "g3_friction")] + [("g3_ground", C.c_int32)]
+                                          "g3_friction")] + [("g3_ground", C.c_int32), ("friction_mode", C.c_int32)]
 
 
 class WgBatch(C.Structure):
@@ -40,7 +40,7 @@ class WgBatch(C.Structure):
                 ("inc", _vp), ("inc_off", _vp),
                 ("muscle_x", _vp), ("muscle_bounds", _vp), ("muscle_stride", _vp),
                 ("steps", _vp), ("contact", _vp), ("pinned", _vp),
-                ("charge", _vp), ("radius", _vp)]
+                ("charge", _vp), ("radius", _vp), ("row", _vp)]
 
 
 class WgOutputs(C.Structure):
@@ -54,7 +54,7 @@ class WgLaunchInfo(C.Structure):
 
 
 EXPORTS = ("wg_abi_version", "wg_last_error", "wg_step", "wg_observe", "wg_reset", "wg_reset_noise",
-           "wg_plan_ragged", "wg_launch_geometry")
+           "wg_plan_ragged", "wg_plan_waves", "wg_wave_edge_passes", "wg_launch_geometry")
 
 _lib = None
 _lock = threading.Lock()
@@ -84,8 +84,11 @@ def load(path: str | None = None):
         L.wg_reset.argtypes = [C.POINTER(WgBatch), C.POINTER(WgParams), _vp, _vp, _vp]
         L.wg_reset_noise.argtypes = [C.POINTER(WgBatch), _vp, _vp]
         L.wg_plan_ragged.argtypes = [_vp, _vp, _vp, C.c_int32, _vp, C.c_int32]
+        L.wg_plan_waves.argtypes = [_vp, _vp, _vp, C.c_int32, _vp, C.c_int32]
+        L.wg_wave_edge_passes.argtypes = [C.c_int32, C.c_int32]
         L.wg_launch_geometry.argtypes = [C.POINTER(WgBatch), C.POINTER(WgLaunchInfo)]
-        for f in ("wg_step", "wg_observe", "wg_reset", "wg_reset_noise", "wg_plan_ragged", "wg_launch_geometry"):
+        for f in ("wg_step", "wg_observe", "wg_reset", "wg_reset_noise", "wg_plan_ragged", "wg_plan_waves",
+                  "wg_wave_edge_passes", "wg_launch_geometry"):
             getattr(L, f).restype = C.c_int
         v = L.wg_abi_version()
         if v != ABI_VERSION:

@@ -59,6 +59,7 @@ class EnvParams:
     g3_restitution: float = 0.8
     g3_friction: float = 0.5
     g3_ground: int = 1
+    friction_mode: int = 0        # 0: gym/optimized_env.py:168-172 friction; 1: the G1 env's (gym/env.py:41)
 
     def to_struct(self) -> _lib.WgParams:
         d = asdict(self)
@@ -71,8 +72,41 @@ class EnvParams:
             raise ValueError("g3_gravity must have 3 components")
         return _lib.WgParams(g3_gravity=(C.c_double * 3)(*gv),
                              **{k: (int(v) if k in ("in3d", "max_steps", "midform", "conmid", "spring_mode",
-                                                    "action_mode", "integrator", "pair_mode", "g3_ground")
+                                                    "action_mode", "integrator", "pair_mode", "g3_ground",
+                                                    "friction_mode")
                                     else float(v)) for k, v in d.items()})
+
+
+def require_tensor(t, name: str, device, dtype, shape=None) -> None:
+    """Refuse a tensor whose raw pointer the kernel cannot use as given: another device (host memory or another
+    GPU), another dtype, a non-contiguous layout or a wrong shape.  Raises ValueError before any launch."""
+    if not isinstance(t, torch.Tensor):
+        raise ValueError(f"{name} must be a torch tensor on {device}")
+    if t.device != torch.device(device):
+        raise ValueError(f"{name} is on {t.device}, the batch is on {device}")
+    if t.dtype != dtype:
+        raise ValueError(f"{name} has dtype {t.dtype}, expected {dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if shape is not None and tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name} has shape {tuple(t.shape)}, expected {tuple(shape)}")
+
+
+class WalkerGraph:
+    """A captured run() (BatchedPhysicsEnv.graph).  The graph holds raw pointers to the env's state and output
+    tensors and the parameters as they were at capture: set_params / a reallocation of the outputs / enabling
+    radii bump the env's generation, and replay() of a graph captured before that raises instead of writing
+    into freed memory or silently stepping with stale parameters."""
+
+    def __init__(self, env: "BatchedPhysicsEnv", graph, actions):
+        self._env, self._graph, self._gen = env, graph, env._generation
+        self.actions = actions            # kept alive: the graph reads it on every replay
+
+    def replay(self) -> None:
+        if self._env._generation != self._gen:
+            raise RuntimeError("stale WalkerGraph: the env's parameters or buffers changed after capture; "
+                               "capture a new graph")
+        self._graph.replay()
 
 
 class BatchedPhysicsEnv:
@@ -83,6 +117,8 @@ class BatchedPhysicsEnv:
         if device is None:
             raise RuntimeError("BatchedPhysicsEnv needs a ROCm GPU (libwalker_hip.so); there is no CPU path")
         device = torch.device(device)
+        if device.type == "cuda" and device.index is None:
+            device = torch.device("cuda", torch.cuda.current_device())
         _lib.load()   # fail loudly before allocating anything
         self.params = EnvParams(**params)
         self.sigma = float(rand_sigma)
@@ -98,6 +134,7 @@ class BatchedPhysicsEnv:
         self._gen = torch.Generator(device=device)
         if seed is not None:
             self._gen.manual_seed(int(seed))
+        self._generation = 0
         self._alloc_outputs()
 
     @classmethod
@@ -129,6 +166,7 @@ class BatchedPhysicsEnv:
 
     # ------------------------------------------------------------------ plumbing
     def _alloc_outputs(self):
+        self._generation += 1
         N, D, dv = self.N, self.obs_dim, self.device
         self.obs = torch.zeros((N, D), dtype=torch.float32, device=dv)
         self.reward = torch.zeros(N, dtype=torch.float32, device=dv)
@@ -156,6 +194,7 @@ class BatchedPhysicsEnv:
         if int(self.params.pair_mode) & 4:
             self.batch.enable_radius()
         self._pstruct = self.params.to_struct()
+        self._generation += 1   # graphs captured before this replay stale parameters: WalkerGraph refuses them
 
     def _check_action(self, action):
         if action is None:
@@ -193,9 +232,9 @@ class BatchedPhysicsEnv:
         obs_out = torch.empty((T, self.N, self.obs_dim), dtype=torch.float32, device=dv) if obs_out is None else obs_out
         reward_out = torch.empty((T, self.N), dtype=torch.float32, device=dv) if reward_out is None else reward_out
         done_out = torch.empty((T, self.N), dtype=torch.uint8, device=dv) if done_out is None else done_out
-        if tuple(obs_out.shape) != (T, self.N, self.obs_dim) or tuple(reward_out.shape) != (T, self.N) or \
-                tuple(done_out.shape) != (T, self.N):
-            raise ValueError("rollout outputs must be [T, N, D] / [T, N] / [T, N]")
+        require_tensor(obs_out, "obs_out", dv, torch.float32, (T, self.N, self.obs_dim))
+        require_tensor(reward_out, "reward_out", dv, torch.float32, (T, self.N))
+        require_tensor(done_out, "done_out", dv, torch.uint8, (T, self.N))
         lanes = self._lanes(lanes) if T > 0 else 1
         if lanes > 1:
             self._run_lanes(actions, T, lambda w0, w1: self._outputs(
@@ -214,8 +253,11 @@ class BatchedPhysicsEnv:
     def run(self, actions, n_steps: int, info: bool = True, lanes: Optional[int] = None):
         """Throughput path: n_steps env steps in one C call; step s acts with actions[s % T]
         ([T, N, A] device tensor; T == n_steps or 1) and overwrites obs/reward/done(/info) each step."""
+        require_tensor(actions, "actions", self.device, torch.float32)
+        if actions.dim() != 3:
+            raise ValueError("actions must be a contiguous [n_steps or 1, N, A] device tensor")
         T, n, cols = actions.shape
-        if n != self.N or T not in (1, n_steps) or not actions.is_contiguous():
+        if n != self.N or T not in (1, n_steps):
             raise ValueError("actions must be a contiguous [n_steps or 1, N, A] device tensor")
         lanes = self._lanes(lanes)
         if lanes > 1:
@@ -253,11 +295,8 @@ class BatchedPhysicsEnv:
         the WgOutputs of walkers [w0, w1)."""
         T, n, cols = actions.shape
         cur = torch.cuda.current_stream(self.device)
-        prio = int(os.environ.get("WG_LANES_PRIO", "0"))   # experiments: side-stream priority (torch: -1 high)
-        key = (lanes, prio)
-        if getattr(self, "_side_key", None) != key:
-            self._side = [torch.cuda.Stream(device=self.device, priority=prio) for _ in range(lanes - 1)]
-            self._side_key = key
+        if len(getattr(self, "_side", [])) != lanes - 1:
+            self._side = [torch.cuda.Stream(device=self.device) for _ in range(lanes - 1)]
         start = torch.cuda.Event()
         start.record(cur)
         L = _lib.load()
@@ -266,11 +305,7 @@ class BatchedPhysicsEnv:
             nb = self.batch.plan_blocks
             bounds = [nb * i // lanes for i in range(lanes)] + [nb]
         else:
-            f0 = float(os.environ.get("WG_LANES_SPLIT", "0"))   # experiments: first range's share (lanes 2)
-            if lanes == 2 and 0.0 < f0 < 1.0:
-                bounds = [0, min(self.N - 64, max(64, (int(self.N * f0) + 63) // 64 * 64)), self.N]
-            else:
-                bounds = [0] + [((self.N * i // lanes) + 63) // 64 * 64 for i in range(1, lanes)] + [self.N]
+            bounds = [0] + [((self.N * i // lanes) + 63) // 64 * 64 for i in range(1, lanes)] + [self.N]
         done = []
         for i in range(lanes):
             w0, w1 = bounds[i], bounds[i + 1]
@@ -297,9 +332,10 @@ class BatchedPhysicsEnv:
 
     def graph(self, actions, n_steps: int, info: bool = True, lanes: Optional[int] = None):
         """Capture run(actions, n_steps) into a HIP graph (torch.cuda.CUDAGraph over the ROCm runtime) and
-        return it; graph.replay() then advances the batch n_steps with one host call, the two walker ranges'
-        streams forked and joined inside the graph.  `actions` must stay alive (and may be refilled in place)
-        while the graph is used; the graph reads the batch and output tensors this env owns."""
+        return it as a WalkerGraph; replay() then advances the batch n_steps with one host call, the two walker
+        ranges' streams forked and joined inside the graph.  `actions` is kept alive by the WalkerGraph (and may be
+        refilled in place); the graph reads the batch and output tensors this env owns and the parameters as
+        captured, so set_params() (or any reallocation of the outputs) makes replay() raise."""
         g = torch.cuda.CUDAGraph()
         side = torch.cuda.Stream(device=self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
@@ -307,7 +343,7 @@ class BatchedPhysicsEnv:
             with torch.cuda.graph(g, stream=side):
                 self.run(actions, n_steps, info=info, lanes=lanes)
         torch.cuda.current_stream(self.device).wait_stream(side)
-        return g
+        return WalkerGraph(self, g, actions)
 
     def observe(self):
         o = self._outputs(self.obs, self.reward, self.done, self.centroid, self.energy)
@@ -322,10 +358,11 @@ class BatchedPhysicsEnv:
         ``noise`` [P, 3] overrides the device generator (use it for reproducible parity runs)."""
         if noise is None and self.sigma > 0:
             noise = torch.randn((self.batch.P, 3), generator=self._gen, device=self.device) * self.sigma
-        if noise is not None:
-            noise = torch.as_tensor(noise, dtype=torch.float32).to(self.device).reshape(self.batch.P, 3).contiguous()
+        if noise is not None:   # caller's mass order -> the stored order
+            noise = self.batch.to_stored("mass", torch.as_tensor(noise, dtype=torch.float32).to(self.device)
+                                         .reshape(self.batch.P, 3)).contiguous()
         if mask is not None:
-            mask = torch.as_tensor(mask).to(self.device, torch.uint8).contiguous()
+            mask = self.batch.to_stored("walker", torch.as_tensor(mask).to(self.device, torch.uint8)).contiguous()
         _lib.check(_lib.load().wg_reset(
             C.byref(self.batch.struct), C.byref(self._pstruct),
             None if noise is None else C.c_void_p(noise.data_ptr()),
@@ -338,28 +375,33 @@ class BatchedPhysicsEnv:
         return [seed] if seed is not None else []
 
     def info(self) -> dict:
-        return {"steps": self.batch.steps, "centroid_position": self.centroid, "total_energy": self.energy}
+        return {"steps": self.batch.caller("steps"), "centroid_position": self.centroid, "total_energy": self.energy}
 
-    # state accessors (device tensors, views into the batch)
+    # state accessors in the caller's order: live views into the batch, or gathered copies for a ragged batch
+    # (stored sorted by size; write through batch.to_stored / batch.stored_mass)
     @property
     def pos(self):
-        return self.batch.pos
+        return self.batch.caller("pos")
 
     @property
     def vel(self):
-        return self.batch.vel
+        return self.batch.caller("vel")
 
     @property
     def acc(self):
-        return self.batch.acc
+        return self.batch.caller("acc")
 
     @property
     def muscle_x(self):
-        return self.batch.muscle_x
+        return self.batch.caller("muscle_x")
 
     @property
     def contact(self):
-        return self.batch.contact
+        return self.batch.caller("contact")
+
+    @property
+    def steps(self):
+        return self.batch.caller("steps")
 
     def get_action_space(self) -> dict:
         return {"shape": (self.batch.A,), "type": "continuous", "low": -1.0, "high": 1.0}

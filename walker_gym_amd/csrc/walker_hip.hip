@@ -55,18 +55,6 @@ constexpr int MAXT = 256;               // __launch_bounds__: workgroups are 64.
 #ifndef WG_ABLATE
 #define WG_ABLATE 0   // profiling builds only (scripts/ablate.py): bit k skips phase k; 0 in the product
 #endif
-// Diagnostic build only (-DWG_STAMPS): thread 0 of each workgroup records s_memrealtime (100 MHz) at
-// phase boundaries into g_stamps[block][8]; read back with wg_debug_stamps().  Never in the product.
-#ifdef WG_STAMPS
-__device__ unsigned long long g_stamps[65536 * 16];
-#define STAMP(k)                                                                                    \
-    do {                                                                                            \
-        if (threadIdx.x == 0 && blockIdx.x < 65536)                                                 \
-            g_stamps[blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memrealtime();                      \
-    } while (0)
-#else
-#define STAMP(k) do {} while (0)
-#endif
 
 // Float32 constants derived from wg_params exactly where numpy rounds the Python scalars.
 struct KParams {
@@ -82,10 +70,9 @@ struct KParams {
     // spring_mode 2, the G3 engine (gym/optimized_walker/env.py:135-184), everything rounded to float32
     float g3g[3], g3_damp, g3_dragc, g3_level, g3_rest, g3_fric;   // g3_dragc = f32(-0.5 * air_resistance)
     int g3_ground;
+    int friction_mode;   // 0: (-v)*(|deep|*friction) (gym/optimized_env.py:168-172); 1: (v*deep)*friction (gym/env.py:41)
     int prio;         // WG_LEAN_PRIO: 1 (default) raise the wave priority while a lean tile issues its loads, so a
-                      // wave's HBM requests leave before other waves' arithmetic; 0 off; 2 (experiment) raise it
-                      // from the loads to the end of the tile (oldest first).  scripts/lean_ab.py, DESIGN §7
-    int stagger;    // diagnostics (WG_STAGGER): blocks with blockIdx % 4 == k idle k*stagger*64 cycles first
+                      // wave's HBM requests leave before other waves' arithmetic; 0 off
 };
 
 // Per-launch geometry: caps of one workgroup's slice (LDS carve sizes).
@@ -96,7 +83,6 @@ struct Geo {
     float invM, invK, invA;    // uniform batches: 1/M, 1/K, 1/A for exact small-int division (fdiv)
     int tbytes;                // spring-term region, also the obs tile of uniform batches (aliased)
     int lite;                  // register-reduction kernels: no LDS for acc, m, reduction terms, offsets
-    int stage;                 // streaming kernel: df region doubles as the pos/vel/acc out-staging tile
 };
 
 struct Carve {
@@ -112,6 +98,9 @@ struct Carve {
 
 __host__ __device__ inline int align16(int b) { return (b + 15) & ~15; }
 
+// the caller's index of stored walker w (its action row and output row; wg_batch.row, NULL = identity)
+__device__ __forceinline__ int caller_row(const wg_batch &b, int w) { return b.row ? b.row[w] : w; }
+
 // one carve for host sizing and device pointers.  The walk produces byte OFFSETS only; the device
 // pointers are `smem + offset` with no null test in between, so the compiler keeps them in the LDS
 // address space (a `base ? base + b : nullptr` select made them generic: flat loads/stores and the
@@ -124,7 +113,7 @@ __host__ __device__ inline int carve_walk(const Geo &g, int *off) {
     const int full = g.lite ? 0 : 1;
     take(g.tbytes); take(g.Pcap * 12); take(g.Pcap * 12);                  // t, pos, vel
     take(full * g.Pcap * 12); take(full * g.Pcap * 4);                      // acc, m
-    take(std::max(g.Ecap * 12, g.stage * g.Pcap * 36));                    // df (streaming kernel: also the out-stage)
+    take(g.Ecap * 12);                                                      // df
     take(g.Ecap * 4 + 16); take(g.Ucap * 4);                                // inc, x
     take(full * g.Pcap * 4); take(full * g.Pcap * 4); take(full * g.Pcap * 4);   // nrm, ke, pe
     take(full * g.W * 32);                                                  // red
@@ -340,10 +329,34 @@ __device__ __forceinline__ void spring_edge(const EdgeRec &e, int le, int lm, fl
 
 // One incidence entry's spring term (float64) and damping force (float32), read from LDS.
 struct IncTerm { double t0, t1, t2; float f0, f1, f2; };
-__device__ __forceinline__ IncTerm inc_term(const double *st, const float *sdf, int lb, int ent) {
-    const int le = lb + (ent >> 1);
-    return IncTerm{st[3 * le], st[3 * le + 1], st[3 * le + 2], sdf[3 * le], sdf[3 * le + 1], sdf[3 * le + 2]};
-}
+// Spring-term storage of a tile in LDS.  TermsAoS: t[3 le + c] (float64), df[3 le + c] (float32) — the
+// workgroup kernel.  TermsSoA: three float64 planes and three float32 planes of `pl` entries — the lean
+// kernels: the edge lanes' stores are then consecutive (conflict-free) instead of a 24-B lane stride.
+struct TermsAoS {
+    double *t;
+    float *f;
+    __device__ __forceinline__ IncTerm get(int le) const {
+        return IncTerm{t[3 * le], t[3 * le + 1], t[3 * le + 2], f[3 * le], f[3 * le + 1], f[3 * le + 2]};
+    }
+    __device__ __forceinline__ void put(int le, double t0, double t1, double t2, float f0, float f1, float f2) const {
+        t[3 * le] = t0; t[3 * le + 1] = t1; t[3 * le + 2] = t2;
+        f[3 * le] = f0; f[3 * le + 1] = f1; f[3 * le + 2] = f2;
+    }
+};
+struct TermsSoA {
+    double *t;
+    float *f;
+    int pl;
+    __device__ __forceinline__ IncTerm get(int le) const {
+        return IncTerm{t[le], t[pl + le], t[2 * pl + le], f[le], f[pl + le], f[2 * pl + le]};
+    }
+    __device__ __forceinline__ void put(int le, double t0, double t1, double t2, float f0, float f1, float f2) const {
+        t[le] = t0; t[pl + le] = t1; t[2 * pl + le] = t2;
+        f[le] = f0; f[pl + le] = f1; f[2 * pl + le] = f2;
+    }
+};
+template <class TS>
+__device__ __forceinline__ IncTerm inc_term(const TS &ts, int lb, int ent) { return ts.get(lb + (ent >> 1)); }
 // a = f32(f64(a) + t/m) (Point.forced with a float64 force, engine.py:67,75), then the damping pair
 // p1.forced(-df), p2.forced(df) (optimized_walker.py:105-106); end j sees the opposite signs.
 __device__ __forceinline__ void acc_f64_entry(const IncTerm &q, int ent, double md, double ym, float mf, float ymf,
@@ -378,7 +391,10 @@ __device__ __forceinline__ void mass_tail(const KParams &kp, float mf, float ymf
         ax = ax + zm; ay = ay + fdiv_mk(kp.neg_groundk * deep, mf, ymf); az = az + zm;
         ax = ax + zm; ay = ay + fdiv_mk(kp.neg_grounddamp * vy, mf, ymf); az = az + zm;
         const float ff = fabsf(deep) * kp.friction;                  // :168
-        ax = ax + fdiv_mk((-vx) * ff, mf, ymf); ay = ay + zm; az = az + fdiv_mk((-vz) * ff, mf, ymf);
+        // G1 env (gym/env.py:41): [v_x*deep*friction, 0, v_z*deep*friction], left to right in float32
+        const float fx = kp.friction_mode ? (vx * deep) * kp.friction : (-vx) * ff;
+        const float fz = kp.friction_mode ? (vz * deep) * kp.friction : (-vz) * ff;
+        ax = ax + fdiv_mk(fx, mf, ymf); ay = ay + zm; az = az + fdiv_mk(fz, mf, ymf);
     }
     if (pinned) { ax = 0.f; ay = 0.f; az = 0.f; }   // DingPoint.forced is a no-op: a stays zeros()
     // v += a*t in both integrators; the position update differs.  Both forms are computed and one selected:
@@ -399,14 +415,13 @@ __device__ __forceinline__ void mass_tail(const KParams &kp, float mf, float ymf
 // per edge — gym/optimized_walker.py:124-127 with gym/engine.py:65-76, 101-102), then gravity, linear
 // damping and the ground penalty (gym/env.py:31-41 / gym/optimized_env.py:146-172, each one
 // Point.forced), then Point.run1 (gym/engine.py:174-178).  Returns the new state and old_a.
-__device__ __forceinline__ void mass_accumulate(const double *st, const float *sdf, const uint16_t *inc, int lb,
-                                                int s0, int s1, float mf, float &ax, float &ay, float &az,
-                                                int spring_mode) {
+template <class TS>
+__device__ __forceinline__ void mass_accumulate(const TS &ts, const uint16_t *inc, int lb, int s0, int s1, float mf,
+                                                float &ax, float &ay, float &az, int spring_mode) {
     const double md = (double)mf;
     const double ym = 1.0 / md;      // one IEEE division per mass; every /m below is exact from it
     const float ymf = (float)ym;     // = RN32(1/m)
     ax = 0.f; ay = 0.f; az = 0.f;
-    STAMP(10);
     // Both ends of an edge see the same spring term t and damping force df with opposite signs; the
     // divisions are odd functions (RN is sign-symmetric), so the quotient is formed once and its sign
     // flipped by one XOR: -(t/m) == (-t)/m exactly, a + (-d) == a - d.
@@ -415,15 +430,14 @@ __device__ __forceinline__ void mass_accumulate(const double *st, const float *s
             const int ent = inc[r];
             const int le = lb + (ent >> 1);
             const uint32_t sj = (uint32_t)(ent & 1) << 31;   // sign of the spring term at this end
-            const double *t = st + 3 * le;
-            const float *f = sdf + 3 * le;
-            ax = ax + fxsign(fdiv_mk((float)t[0], mf, ymf), sj);
-            ay = ay + fxsign(fdiv_mk((float)t[1], mf, ymf), sj);
-            az = az + fxsign(fdiv_mk((float)t[2], mf, ymf), sj);
+            const IncTerm q = ts.get(le);
+            ax = ax + fxsign(fdiv_mk((float)q.t0, mf, ymf), sj);
+            ay = ay + fxsign(fdiv_mk((float)q.t1, mf, ymf), sj);
+            az = az + fxsign(fdiv_mk((float)q.t2, mf, ymf), sj);
             const uint32_t sd = sj ^ 0x80000000u;          // damping: p1 gets -df, p2 gets +df
-            ax = ax + fxsign(fdiv_mk(f[0], mf, ymf), sd);
-            ay = ay + fxsign(fdiv_mk(f[1], mf, ymf), sd);
-            az = az + fxsign(fdiv_mk(f[2], mf, ymf), sd);
+            ax = ax + fxsign(fdiv_mk(q.f0, mf, ymf), sd);
+            ay = ay + fxsign(fdiv_mk(q.f1, mf, ymf), sd);
+            az = az + fxsign(fdiv_mk(q.f2, mf, ymf), sd);
         }
     } else {
         // Fast path: the Markstein quotients without their non-finite guards.  They differ from the
@@ -436,14 +450,14 @@ __device__ __forceinline__ void mass_accumulate(const double *st, const float *s
         if (s1 > s0) {
             const int rl = s1 - 1;
             int ea = inc[s0], eb = inc[min(s0 + 1, rl)];
-            IncTerm A = inc_term(st, sdf, lb, ea), B;
+            IncTerm A = inc_term(ts, lb, ea), B;
             for (int r = s0; r < s1; r += 2) {
-                B = inc_term(st, sdf, lb, eb);
+                B = inc_term(ts, lb, eb);
                 const int ea2 = inc[min(r + 2, rl)];
                 __builtin_amdgcn_sched_barrier(0);   // keep the reads above the arithmetic
                 acc_f64_entry(A, ea, md, ym, mf, ymf, ax, ay, az);
                 if (r + 1 >= s1) break;
-                A = inc_term(st, sdf, lb, ea2);
+                A = inc_term(ts, lb, ea2);
                 const int eb2 = inc[min(r + 3, rl)];
                 __builtin_amdgcn_sched_barrier(0);
                 acc_f64_entry(B, eb, md, ym, mf, ymf, ax, ay, az);
@@ -452,7 +466,6 @@ __device__ __forceinline__ void mass_accumulate(const double *st, const float *s
                 asm volatile("" : "+v"(A.t0), "+v"(A.t1), "+v"(A.t2), "+v"(A.f0), "+v"(A.f1), "+v"(A.f2), "+v"(ea), "+v"(eb));
             }
         }
-        STAMP(7);
         const bool bad = !(__builtin_isfinite(ax) && __builtin_isfinite(ay) && __builtin_isfinite(az));
         if (__builtin_expect(bad, 0)) {
             ax = 0.f; ay = 0.f; az = 0.f;
@@ -460,15 +473,14 @@ __device__ __forceinline__ void mass_accumulate(const double *st, const float *s
                 const int ent = inc[r];
                 const int le = lb + (ent >> 1);
                 const uint32_t sj = (uint32_t)(ent & 1) << 31;
-                const double *t = st + 3 * le;
-                const float *f = sdf + 3 * le;
-                ax = (float)((double)ax + dxsign(t[0] / md, sj));
-                ay = (float)((double)ay + dxsign(t[1] / md, sj));
-                az = (float)((double)az + dxsign(t[2] / md, sj));
+                const IncTerm q = ts.get(le);
+                ax = (float)((double)ax + dxsign(q.t0 / md, sj));
+                ay = (float)((double)ay + dxsign(q.t1 / md, sj));
+                az = (float)((double)az + dxsign(q.t2 / md, sj));
                 const uint32_t sd = sj ^ 0x80000000u;
-                ax = ax + fxsign(f[0] / mf, sd);
-                ay = ay + fxsign(f[1] / mf, sd);
-                az = az + fxsign(f[2] / mf, sd);
+                ax = ax + fxsign(q.f0 / mf, sd);
+                ay = ay + fxsign(q.f1 / mf, sd);
+                az = az + fxsign(q.f2 / mf, sd);
             }
         }
     }
@@ -517,7 +529,8 @@ __device__ __forceinline__ void mass_step(const KParams &kp, const double *st, c
         g3_mass_step(kp, st, inc, lb, s0, s1, mf, p3, v3, px, py, pz, vx, vy, vz, ax, ay, az, hit, pinned);
         return;
     }
-    mass_accumulate(st, sdf, inc, lb, s0, s1, mf, ax, ay, az, spring_mode);
+    mass_accumulate(TermsAoS{const_cast<double *>(st), const_cast<float *>(sdf)}, inc, lb, s0, s1, mf, ax, ay, az,
+                    spring_mode);
     const float ymf = (float)(1.0 / (double)mf);
     mass_tail(kp, mf, ymf, p3, v3, px, py, pz, vx, vy, vz, ax, ay, az, hit, pinned);
 }
@@ -573,6 +586,56 @@ __device__ inline float pw_sum_lanes(float x, int base, int M, int lane) {
     return r;
 }
 
+// ------------------------------------------------------------------ pair passes from LDS (workgroup kernel)
+// SURVEY §8(f) 3 for walkers the lean kernel does not take (M not dividing 64, M > 64, ragged batches): the
+// arithmetic of pair_central / pair_bounce (lean kernel, below) with the partners' positions read from the tile's
+// LDS copy, unchanged until every mass of the tile has accumulated (walker_step_kernel puts a barrier there).
+// Mass q of the walker whose masses are LDS [lm, lm + M) and global [g0, g0 + M).
+__device__ void pair_forces_lds(const wg_batch &b, const KParams &kp, const float *spos, const float *sm, int lm,
+                                int M, int q, size_t g0, float mf, float &ax, float &ay, float &az) {
+    const float *p3 = spos + 3 * (lm + q);
+    const double md = (double)mf;
+    for (int pass = 0; pass < 2; pass++) {   // gym/engine.py:128-137 (Config.g, m) and :139-147 (Config.k, e)
+        if (!(kp.pair_mode & (1 << pass))) continue;
+        const double coef = pass == 0 ? kp.pair_g : kp.pair_k;
+        const double sq = pass == 0 ? md : (b.charge ? b.charge[g0 + q] : kp.pair_e);
+        for (int pj = 0; pj < M; pj++) {
+            if (pj == q) continue;
+            const float *o3 = spos + 3 * (lm + pj);
+            const double os = pass == 0 ? (double)sm[lm + pj] : (b.charge ? b.charge[g0 + pj] : kp.pair_e);
+            const float d0 = o3[0] - p3[0], d1 = o3[1] - p3[1], d2 = o3[2] - p3[2];   // partner - self
+            double r = (double)np_norm3(d0, d1, d2);
+            if (CONFIG_R > r) r = CONFIG_R;
+            const double slo = pj < q ? os : sq, shi = pj < q ? sq : os;
+            const double f = ((-coef) * slo) * shi / (r * r);
+            ax = (float)((double)ax + ((-f) * (double)d0 / r) / md);
+            ay = (float)((double)ay + ((-f) * (double)d1 / r) / md);
+            az = (float)((double)az + ((-f) * (double)d2 / r) / md);
+        }
+    }
+    if (kp.pair_mode & 4) {                  // gym/engine.py:114-125, partners j < q, then j != q, then j > q
+        const double rs = b.radius[g0 + q];
+        for (int ph = 0; ph < 3; ph++) {
+            for (int pj = 0; pj < M; pj++) {
+                const bool on = ph == 0 ? pj < q : ph == 1 ? pj != q : pj > q;
+                if (!on) continue;
+                const float *o3 = spos + 3 * (lm + pj);
+                const float d0 = o3[0] - p3[0], d1 = o3[1] - p3[1], d2 = o3[2] - p3[2];
+                const float cur = np_norm3(d0, d1, d2);
+                const double x = rs + b.radius[g0 + pj];
+                if (!((double)cur <= x)) continue;
+                const float dx = cur - (float)x;                                  // engine.py:96
+                const float nf = -((-dx) * kp.bounce_kh);                         // -f_size, :75,100
+                double dist = (double)cur;
+                if (CONFIG_R > dist) dist = CONFIG_R;
+                ax = (float)((double)ax + (double)(nf * d0) / dist / md);
+                ay = (float)((double)ay + (double)(nf * d1) / dist / md);
+                az = (float)((double)az + (double)(nf * d2) / dist / md);
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------------ the step kernel
 // STEP = false: observe only (reset path).  RAGGED: CSR offsets + block plan.  IN3D: obs layout.
 // PWD: pairwise-sum recursion depth (0: M <= 128).  SHFL: register reductions (uniform, M | 64).
@@ -583,11 +646,6 @@ __global__ __launch_bounds__(MAXT) void walker_step_kernel(
     extern __shared__ __attribute__((aligned(16))) char smem[];
     Carve s = carve(smem, geo);
     const int tid = threadIdx.x, lane = tid & 63, T = blockDim.x;
-    if (kp.stagger > 0) {
-        const int k = (int)(blockIdx.x & 3) * kp.stagger;
-        for (int i = 0; i < k; i++) __builtin_amdgcn_s_sleep(1);
-    }
-    STAMP(0);
 
     // ---- this workgroup's walker range and flat slices
     int w0, w1;
@@ -681,7 +739,7 @@ __global__ __launch_bounds__(MAXT) void walker_step_kernel(
                         lo = bd.x; hi = bd.y;
                         if (kp.action_mode == 1) st = b.muscle_stride[U0 + u];
                     }
-                    a = action[(size_t)(w0 + wl) * action_stride + ua];
+                    a = action[(size_t)caller_row(b, w0 + wl) * action_stride + ua];
                 }
                 if (kp.action_mode == 1) x = (a != 0.f) ? x + st : x - st;
                 else x = x + a;
@@ -693,7 +751,6 @@ __global__ __launch_bounds__(MAXT) void walker_step_kernel(
         s.x[u] = x;
     }
     __syncthreads();
-    STAMP(1);
 
     // registers of this lane's (first) mass after the physics: feed the SHFL reductions and obs
     float px = 0.f, py = 0.f, pz = 0.f, vx = 0.f, vy = 0.f, vz = 0.f, ax = 0.f, ay = 0.f, az = 0.f;
@@ -724,29 +781,53 @@ __global__ __launch_bounds__(MAXT) void walker_step_kernel(
             }
         }
         __syncthreads();
-        STAMP(2);
 
         // ================= 3. mass phase: ordered accumulation, env forces, run1 =================
         const uint16_t *s_inc16 = reinterpret_cast<const uint16_t *>(s.inc);
-        for (int lp = tid; lp < nP; lp += T) {
+        // mass lp's walker, its first mass and incidence range
+        auto mass_of = [&](int lp, int &wl, int &lm, int &s0, int &s1) {
             const bool first = (lp == tid);
-            int wl, lm;
             if (first) { wl = my_wl; lm = my_lm; }
             else if (RAGGED) { wl = locate(s.moff, nw, lp); lm = s.moff[wl]; }
             else { wl = fdiv(lp, b.M, geo.invM); lm = wl * b.M; }
-            const int lb = RAGGED ? s.eoff[wl] : wl * b.K;
-            int s0 = io0, s1 = io1;
+            s0 = io0; s1 = io1;
             if (!first) {
                 const uint16_t *io = b.inc_off + (size_t)(P0 + lm) + (size_t)(w0 + wl);
                 s0 = io[lp - lm]; s1 = io[lp - lm + 1];
             }
+        };
+        const bool pairs = !SHFL && kp.pair_mode != 0;   // block-uniform
+        if (pairs) {
+            // pair passes read the other masses' positions: every mass accumulates its springs
+            // and pair terms first (into s.acc), the env forces and the integrator follow after a barrier
+            for (int lp = tid; lp < nP; lp += T) {
+                int wl, lm, s0, s1;
+                mass_of(lp, wl, lm, s0, s1);
+                const int lb = RAGGED ? s.eoff[wl] : wl * b.K;
+                const int M = RAGGED ? s.moff[wl + 1] - lm : b.M;
+                const float mf = s.m[lp];
+                mass_accumulate(TermsAoS{s.t, s.df}, s_inc16 + 2 * lb, lb, s0, s1, mf, ax, ay, az, 0);
+                pair_forces_lds(b, kp, s.pos, s.m, lm, M, lp - lm, (size_t)P0 + lm, mf, ax, ay, az);
+                s.acc[3 * lp] = ax; s.acc[3 * lp + 1] = ay; s.acc[3 * lp + 2] = az;
+            }
+            __syncthreads();
+        }
+        for (int lp = tid; lp < nP; lp += T) {
+            int wl, lm, s0, s1;
+            mass_of(lp, wl, lm, s0, s1);
+            const int lb = RAGGED ? s.eoff[wl] : wl * b.K;
             const float mf = SHFL ? my_m : s.m[lp];
             const double md = (double)mf;
             bool hit;
-            mass_step(kp, s.t, s.df, s_inc16 + 2 * lb, lb, s0, (WG_ABLATE & 2) ? min(s1, s0 + 1) : s1, mf,
-                      s.pos + 3 * lp, s.vel + 3 * lp, px, py, pz, vx, vy, vz, ax, ay, az, hit, kp.spring_mode,
-                      b.pinned && b.pinned[P0 + lp]);
-            STAMP(8);
+            if (pairs) {
+                ax = s.acc[3 * lp]; ay = s.acc[3 * lp + 1]; az = s.acc[3 * lp + 2];
+                mass_tail(kp, mf, (float)(1.0 / md), s.pos + 3 * lp, s.vel + 3 * lp, px, py, pz, vx, vy, vz, ax, ay,
+                          az, hit, b.pinned && b.pinned[P0 + lp]);
+            } else {
+                mass_step(kp, s.t, s.df, s_inc16 + 2 * lb, lb, s0, (WG_ABLATE & 2) ? min(s1, s0 + 1) : s1, mf,
+                          s.pos + 3 * lp, s.vel + 3 * lp, px, py, pz, vx, vy, vz, ax, ay, az, hit, kp.spring_mode,
+                          b.pinned && b.pinned[P0 + lp]);
+            }
             if (b.contact) b.contact[P0 + lp] = (uint8_t)hit;
             if (b.radius) b.radius[P0 + lp] = hit ? 3.0 : 1.0;   // gym/optimized_env.py:156,175
             s.pos[3 * lp] = px; s.pos[3 * lp + 1] = py; s.pos[3 * lp + 2] = pz;
@@ -795,7 +876,6 @@ __global__ __launch_bounds__(MAXT) void walker_step_kernel(
         const float ksum = pw_sum_lanes(ke, gbase, M, lane), psum = pw_sum_lanes(pe, gbase, M, lane);
         const unsigned long long gmask = (M == 64) ? ~0ull : (((1ull << M) - 1ull) << (gbase & 63));
         // the collision penalty counts contacts of the NEW state (optimized_env.py:200 runs after run1)
-        STAMP(9);
         const unsigned long long hb = __ballot(is_mass && (py - kp.ground < 0.f));
         const unsigned long long sb = __ballot(is_mass && nv < 0.1f);
         const int hits = __popcll(hb & gmask);
@@ -823,7 +903,6 @@ __global__ __launch_bounds__(MAXT) void walker_step_kernel(
         }
     }
     __syncthreads();
-    STAMP(3);
 
     if (STEP) {
         stage_out(b.pos + 3 * (size_t)P0, s.pos, 3 * nP, tid, T);
@@ -861,19 +940,19 @@ __global__ __launch_bounds__(MAXT) void walker_step_kernel(
             s.red[idx] = v;
         }
         __syncthreads();
-        STAMP(4);
         if (tid < nw) {
             const int wl = tid;
             const int lm = RAGGED ? s.moff[wl] : wl * b.M;
             const int M = RAGGED ? s.moff[wl + 1] - lm : b.M;
-            const size_t wg = (size_t)(w0 + wl);
+            const size_t ws = (size_t)(w0 + wl);             // stored walker (steps)
+            const size_t wg = (size_t)caller_row(b, w0 + wl);   // the caller's row (outputs)
             const float fM = (float)M;
             const float *rd = s.red + 8 * wl;
             const float cy = rd[3] / fM;
             const int packed = __float_as_int(rd[7]);
             const int hits = packed >> 1, all = packed & 1;
             int steps = wsteps;
-            if (STEP) { steps += 1; b.steps[wg] = steps; }
+            if (STEP) { steps += 1; b.steps[ws] = steps; }
             if (o.reward) {
                 const float av = rd[4] / fM;
                 const float vpen = (-av) * 0.1f;
@@ -931,7 +1010,8 @@ __global__ __launch_bounds__(MAXT) void walker_step_kernel(
                 else { wl = fdiv(lp, b.M, geo.invM); lm = wl * b.M; }
                 const int M = RAGGED ? s.moff[wl + 1] - lm : b.M;
                 const float fM = (float)M;
-                float *row = (RAGGED ? ob : tile) + (size_t)wl * stride + per * (lp - lm);
+                float *row = (RAGGED ? o.obs + (size_t)caller_row(b, w0 + wl) * stride : tile + (size_t)wl * stride) +
+                             per * (lp - lm);
 #pragma unroll
                 for (int c = 0; c < d; c++) {
                     const float pv = s.pos[3 * lp + c];
@@ -946,7 +1026,7 @@ __global__ __launch_bounds__(MAXT) void walker_step_kernel(
                 const int lm = RAGGED ? s.moff[wl] : wl * b.M;
                 const int M = RAGGED ? s.moff[wl + 1] - lm : b.M;
                 const int A = RAGGED ? s.uoff[wl + 1] - s.uoff[wl] : b.A;
-                float *row = (RAGGED ? ob : tile) + (size_t)wl * stride;
+                float *row = RAGGED ? o.obs + (size_t)caller_row(b, w0 + wl) * stride : tile + (size_t)wl * stride;
                 if (nmid)
                     for (int c = 0; c < 3; c++)
                         row[per * M + c] = kp.midform == 2 ? s.red[8 * wl + c] : kp.midform ? s.red[8 * wl + c] / (float)M : 0.f;
@@ -958,227 +1038,16 @@ __global__ __launch_bounds__(MAXT) void walker_step_kernel(
             int wl, ua, M;
             if (RAGGED) { wl = locate(s.uoff, nw, u); ua = u - s.uoff[wl]; M = s.moff[wl + 1] - s.moff[wl]; }
             else { wl = fdiv(u, b.A, geo.invA); ua = u - wl * b.A; M = b.M; }
-            (RAGGED ? ob : tile)[(size_t)wl * stride + per * M + nmid + ua] = s.x[u] * kp.mk;
+            (RAGGED ? o.obs + (size_t)caller_row(b, w0 + wl) * stride : tile + (size_t)wl * stride)[per * M + nmid + ua] =
+                s.x[u] * kp.mk;
         }
         if (!RAGGED) {
             __syncthreads();
-            STAMP(5);
             stage_out(ob, tile, nw * stride, tid, T);
         }
     }
-    STAMP(6);
 }
 
-
-// ------------------------------------------------------------------ streaming (persistent) kernel
-// Uniform batches with register reductions (M | 64): persistent workgroups walk tiles of W walkers and
-// keep the NEXT tile's global loads (state, incidence, spring / muscle records) in flight in registers
-// while the current tile computes, so the chip does not alternate between an all-load phase and an
-// all-compute phase (measured phase lock of the one-tile-per-workgroup kernel).
-typedef float vf4 __attribute__((ext_vector_type(4)));   // native vectors keep loop-carried values in VGPRs
-typedef unsigned vu4 __attribute__((ext_vector_type(4)));
-typedef float vf2 __attribute__((ext_vector_type(2)));
-
-// PERSIST = false: one tile per workgroup (grid = tiles), all of the tile's loads issued before any
-// of them is waited on; PERSIST = true: persistent grid with the next tile prefetched (see above).
-template <bool IN3D, int NE, bool PERSIST>
-__global__ __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(4, 8))) void walker_step_stream(
-    wg_batch b, KParams kp, const float *__restrict__ action, int action_cols, int action_stride,
-    wg_outputs o, Geo geo, int ntiles) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const Carve s = carve(smem, geo);
-    const int T = blockDim.x;
-    const int W = geo.W, M = b.M, K = b.K, A = b.A;
-    const int nP = W * M, nE = W * K, nU = W * A;
-    const int n3 = 3 * nP / 4, ni = nE / 4;
-    // Fixed lane roles.  Re-derived inside the tile loop from an opaque copy of the lane id: if they
-    // were loop invariants the compiler would keep ~80 of them live in VGPRs across the whole loop.
-#define WG_LANE_ROLES(tid_expr)                                                                            \
-    const int tid = (tid_expr), lane = tid & 63;                                                            \
-    const bool is_mass = tid < nP, is_mus = tid < nU;                                                       \
-    const int my_wl = fdiv(tid, M, geo.invM), my_q = tid - my_wl * M;                                       \
-    const int gbase = (tid & ~63) + ((lane / M) * M);            /* first lane of my walker in the wave */  \
-    const int mu_wl = A > 0 ? fdiv(tid, A, geo.invA) : 0, mu_ua = tid - mu_wl * A;                          \
-    const bool acts = action != nullptr && is_mus && mu_ua < action_cols;                                   \
-    /* clamped per-lane indices: every prefetch load is unconditional (no branches around loads) */         \
-    const int i3 = min(tid, n3 - 1), ii = min(tid, max(ni - 1, 0));                                         \
-    const int iu = min(tid, max(nU - 1, 0)), iw = min(my_wl, W - 1), iq = min(my_q, M - 1);                 \
-    const int iau = min(mu_ua, max(A - 1, 0)), iaw = min(mu_wl, W - 1);                                     \
-    (void)is_mass; (void)is_mus; (void)acts; (void)gbase; (void)i3; (void)ii; (void)iu; (void)iw; (void)iq;  \
-    (void)iau; (void)iaw
-
-    // prefetch registers: tile t + gridDim.x, loaded while tile t computes
-    vf4 pp, pv; vu4 pi = vu4{0u, 0u, 0u, 0u}; vu4 pe[NE];
-    float pm, pmx = 0.f, pact = 0.f, pst = 0.f; vf2 pbd = vf2{0.f, 0.f};
-    uint32_t pio = 0u; int psteps;
-    // current-tile registers (the records the compute reads outside LDS)
-    vu4 ce[NE];
-    float mf, bx, ba, bst; vf2 bd; uint32_t io; int wsteps;
-#define WG_PREFETCH(tile_)                                                                                  \
-    do {                                                                                                    \
-        const int w0_ = (tile_) * W;                                                                        \
-        const size_t P0_ = (size_t)w0_ * M, E0_ = (size_t)w0_ * K, U0_ = (size_t)w0_ * A;                   \
-        pp = reinterpret_cast<const vf4 *>(b.pos + 3 * P0_)[i3];                                             \
-        pv = reinterpret_cast<const vf4 *>(b.vel + 3 * P0_)[i3];                                             \
-        pm = b.mass[P0_ + min(tid, nP - 1)];                                                                 \
-        if (nE > 0) {                                                                                        \
-            pi = reinterpret_cast<const vu4 *>(reinterpret_cast<const uint32_t *>(b.inc) + E0_)[ii];         \
-            _Pragma("unroll") for (int it = 0; it < NE; it++)                                                \
-                pe[it] = reinterpret_cast<const vu4 *>(b.edges)[E0_ + min(tid + it * T, nE - 1)];            \
-            const uint16_t *io_ = b.inc_off + P0_ + (size_t)w0_ + (size_t)iw * (M + 1) + iq;                 \
-            pio = (uint32_t)io_[0] | ((uint32_t)io_[1] << 16);                                               \
-        }                                                                                                    \
-        if (nU > 0) {                                                                                        \
-            pmx = b.muscle_x[U0_ + iu];                                                                      \
-            if (action) {                                                                                    \
-                pbd = reinterpret_cast<const vf2 *>(b.muscle_bounds)[U0_ + iu];                              \
-                if (kp.action_mode == 1) pst = b.muscle_stride[U0_ + iu];                                    \
-                pact = action[(size_t)(w0_ + iaw) * action_stride + iau];                                    \
-            }                                                                                                \
-        }                                                                                                    \
-        psteps = b.steps[w0_ + iw];                                                                          \
-    } while (0)
-    // commit: prefetched state -> LDS (pos, vel, incidence), records -> current-tile registers
-#define WG_COMMIT()                                                                                         \
-    do {                                                                                                    \
-        if (tid < n3) { reinterpret_cast<vf4 *>(s.pos)[tid] = pp; reinterpret_cast<vf4 *>(s.vel)[tid] = pv; } \
-        if (tid < ni) reinterpret_cast<vu4 *>(s.inc)[tid] = pi;                                              \
-        _Pragma("unroll") for (int it = 0; it < NE; it++) ce[it] = pe[it];                                   \
-        mf = pm; bx = pmx; ba = pact; bst = pst; bd = pbd; io = pio; wsteps = psteps;                       \
-    } while (0)
-
-    int tile = blockIdx.x;
-    if (tile >= ntiles) return;
-    {
-        WG_LANE_ROLES((int)threadIdx.x);
-        WG_PREFETCH(tile);
-        WG_COMMIT();
-        if (PERSIST && tile + (int)gridDim.x < ntiles) WG_PREFETCH(tile + (int)gridDim.x);
-    }
-    // Per tile: compute from LDS + current registers; then commit the (long since landed) prefetch and
-    // issue the next one BEFORE this tile's stores, so no load is ever waited on behind a store.
-    for (; tile < ntiles; tile += PERSIST ? (int)gridDim.x : ntiles) {
-        int tid_opaque = threadIdx.x;
-        asm volatile("" : "+v"(tid_opaque));
-        WG_LANE_ROLES(tid_opaque);
-        const int w0 = tile * W;
-        const size_t P0 = (size_t)w0 * M, U0 = (size_t)w0 * A;
-        const bool has_next = PERSIST && tile + (int)gridDim.x < ntiles;
-        const int steps = wsteps + 1;   // this tile's (wsteps is overwritten by the commit below)
-
-        // ---- act (gym/optimized_walker.py:27-43,164-172)
-        float x = bx;
-        if (acts) {
-            x = (kp.action_mode == 1) ? ((ba != 0.f) ? x + bst : x - bst) : x + ba;
-            if (bd.x > x) x = bd.x;     // Python max(x, originx*minl)
-            if (bd.y < x) x = bd.y;     // Python min(x, originx*maxl)
-        }
-        if (is_mus) s.x[tid] = x;
-        __syncthreads();   // also: the previous tile's stage-out reads of t/df/spos are done
-
-        // ---- edge phase
-        _Pragma("unroll") for (int it = 0; it < NE; it++) {
-            const int le = tid + it * T;
-            if (le < nE) {
-                const EdgeRec e{ce[it].x, __uint_as_float(ce[it].y), __uint_as_float(ce[it].z), __uint_as_float(ce[it].w)};
-                const int wl = fdiv(le, K, geo.invK), ew = le - wl * K;
-                spring_edge(e, le, wl * M, (ew < A) ? s.x[wl * A + ew] : e.rest, s.pos, s.vel, s.t, s.df, kp.spring_mode);
-            }
-        }
-        __syncthreads();
-
-        // ---- mass phase
-        float px = 0.f, py = 0.f, pz = 0.f, vx = 0.f, vy = 0.f, vz = 0.f, ax = 0.f, ay = 0.f, az = 0.f;
-        float nv = 0.f, ke = 0.f, pe_ = 0.f;
-        bool hit = false;
-        if (is_mass) {
-            const int lb = my_wl * K;
-            mass_step(kp, s.t, s.df, reinterpret_cast<const uint16_t *>(s.inc) + 2 * lb, lb, (int)(io & 0xffffu),
-                      (int)(io >> 16), mf, s.pos + 3 * tid, s.vel + 3 * tid, px, py, pz, vx, vy, vz, ax, ay, az, hit,
-                      kp.spring_mode, b.pinned && b.pinned[P0 + tid]);
-            nv = np_norm3(vx, vy, vz);
-            ke = mf * (nv * nv);     // numpy's float32 ** 2 is libm powf: may differ by 1 ulp
-            pe_ = (float)((double)mf * kp.g) * (py - kp.ground);
-        }
-        // per-walker reductions in registers (all lanes of the wave take part in the shuffles)
-        float sx, sy, sz;
-        seq_sum3_lanes(px, py, pz, gbase, M, sx, sy, sz);
-        const float ysum = pw_sum_lanes(py, gbase, M, lane), vsum = pw_sum_lanes(nv, gbase, M, lane);
-        const float ksum = pw_sum_lanes(ke, gbase, M, lane), psum = pw_sum_lanes(pe_, gbase, M, lane);
-        const unsigned long long gmask = (M == 64) ? ~0ull : (((1ull << M) - 1ull) << (gbase & 63));
-        const unsigned long long hb = __ballot(is_mass && (py - kp.ground < 0.f));   // contacts after run1 (:200)
-        const unsigned long long sb = __ballot(is_mass && nv < 0.1f);
-        const float fM = (float)M;
-        const float midx = sx / fM, midy = sy / fM, midz = sz / fM;
-        __syncthreads();     // edge/mass LDS reads done: t, pos, vel, inc are free
-        if (is_mass) {    // out-stage tile in the (now free) damping-force region: pos | vel | acc
-            float *sp = s.df + 3 * tid, *sv = s.df + 3 * nP + 3 * tid, *sa = s.df + 6 * nP + 3 * tid;
-            sp[0] = px; sp[1] = py; sp[2] = pz;
-            sv[0] = vx; sv[1] = vy; sv[2] = vz;
-            sa[0] = ax; sa[1] = ay; sa[2] = az;
-        }
-        if (o.obs) {
-            constexpr int d = IN3D ? 3 : 2, per = 3 * d;
-            const int stride = o.obs_stride, nmid = kp.conmid ? 3 : 0;
-            float *tile_obs = reinterpret_cast<float *>(s.t);
-            if (is_mass) {
-                float *row = tile_obs + (size_t)my_wl * stride + per * my_q;
-                const float pm3[3] = {px, py, pz}, vm3[3] = {vx, vy, vz}, am3[3] = {ax, ay, az};
-                const float mm3[3] = {kp.midform == 2 ? sx : midx, kp.midform == 2 ? sy : midy, kp.midform == 2 ? sz : midz};
-                _Pragma("unroll") for (int c = 0; c < d; c++) {
-                    row[c] = kp.midform ? (pm3[c] - mm3[c]) * kp.pk : pm3[c] * kp.pk;
-                    row[d + c] = vm3[c] * kp.vk;
-                    row[2 * d + c] = am3[c] * kp.ak;
-                }
-                if (my_q == 0) {
-                    float *wrow = tile_obs + (size_t)my_wl * stride;
-                    if (nmid) {
-                        wrow[per * M] = kp.midform ? mm3[0] : 0.f; wrow[per * M + 1] = kp.midform ? mm3[1] : 0.f;
-                        wrow[per * M + 2] = kp.midform ? mm3[2] : 0.f;
-                    }
-                    for (int r = per * M + nmid + A; r < stride; r++) wrow[r] = 0.f;
-                }
-            }
-            if (is_mus) tile_obs[(size_t)mu_wl * stride + per * M + nmid + mu_ua] = x * kp.mk;
-        }
-        // ---- next tile: commit the prefetch (landed during this tile's compute), issue the one after
-        if (has_next) {
-            WG_COMMIT();
-            if (tile + 2 * (int)gridDim.x < ntiles) WG_PREFETCH(tile + 2 * (int)gridDim.x);
-        }
-        __syncthreads();
-        // ---- this tile's stores
-        if (acts) b.muscle_x[U0 + tid] = x;
-        if (is_mass) {
-            if (b.contact) b.contact[P0 + tid] = (uint8_t)hit;
-            if (b.radius) b.radius[P0 + tid] = hit ? 3.0 : 1.0;
-            if (my_q == 0) {                                          // gym/optimized_env.py:189-248
-                const size_t wg = (size_t)(w0 + my_wl);
-                b.steps[wg] = steps;
-                const float cy = ysum / fM;
-                if (o.reward) {
-                    const float vpen = (-(vsum / fM)) * 0.1f;
-                    o.reward[wg] = (cy + vpen) + (float)(-(double)__popcll(hb & gmask) * 0.5);
-                }
-                if (o.done) {
-                    int done = steps >= kp.max_steps;
-                    if (!done && cy < kp.done_y) done = 1;
-                    if (!done && steps > 100) done = (sb & gmask) == gmask;
-                    o.done[wg] = (uint8_t)done;
-                }
-                if (o.centroid) { o.centroid[3 * wg] = midx; o.centroid[3 * wg + 1] = midy; o.centroid[3 * wg + 2] = midz; }
-                if (o.energy) o.energy[wg] = 0.5f * ksum + psum;
-            }
-        }
-        stage_out(b.pos + 3 * P0, s.df, 3 * nP, tid, T);
-        stage_out(b.vel + 3 * P0, s.df + 3 * nP, 3 * nP, tid, T);
-        stage_out(b.acc + 3 * P0, s.df + 6 * nP, 3 * nP, tid, T);
-        if (o.obs) stage_out(o.obs + (size_t)w0 * o.obs_stride, reinterpret_cast<const float *>(s.t), W * o.obs_stride, tid, T);
-    }
-#undef WG_PREFETCH
-#undef WG_COMMIT
-#undef WG_LANE_ROLES
-}
 
 // ------------------------------------------------------------------ lean wave-independent kernel
 // Uniform batches with M | 64 (4 <= M <= 64): one mass per lane, 64/M walkers per wave and NO
@@ -1190,13 +1059,10 @@ __global__ __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(4, 8))) vo
 struct LeanGeo {
     int wpw;                                  // walkers per wave (64 / M)
     int wpb;                                  // waves per workgroup
-    int persist;                              // 0: one tile per wave; 1: persistent waves loop over tiles;
-                                              // 2: persistent, next tile's loads in flight (walker_step_lean_pf)
-    int quo;                                  // 1: per-end quotients formed in the edge phase (lean_compute)
     int lgM;                                  // log2(M)
     int slice;                                // LDS bytes per wave
     int off_df, off_inc, off_x;               // byte offsets in the slice (spring terms / obs tile at 0)
-    int n2;                                   // incidence entries of a full wave tile (2 * wpw * K)
+    int pl;                                   // entries per spring-term plane (SoA; >= wpw * K, even)
     float invK, invA, invM;                   // invM = 1/M, exact (M | 64 is a power of two)
 };
 
@@ -1267,21 +1133,19 @@ __device__ __forceinline__ void spring_terms(const EdgeRec &e, float x, float pi
     const float dkc = dk * e.c;                                               // :104
     g0 = dkc * d0; g1 = dkc * d1; g2 = dkc * d2;
 }
+template <class TS>
 __device__ __forceinline__ void spring_edge_regs(const EdgeRec &e, int le, float x, float pix, float piy, float piz,
                                                  float pjx, float pjy, float pjz, float vix, float viy, float viz,
-                                                 float vjx, float vjy, float vjz, double *st, float *sdf,
-                                                 int spring_mode) {
+                                                 float vjx, float vjy, float vjz, const TS &ts, int spring_mode) {
     double t0, t1, t2;
     float g0, g1, g2;
     spring_terms(e, x, pix, piy, piz, pjx, pjy, pjz, vix, viy, viz, vjx, vjy, vjz, t0, t1, t2, g0, g1, g2, spring_mode);
-    st[3 * le] = t0; st[3 * le + 1] = t1; st[3 * le + 2] = t2;
-    sdf[3 * le] = g0; sdf[3 * le + 1] = g1; sdf[3 * le + 2] = g2;
+    ts.put(le, t0, t1, t2, g0, g1, g2);
 }
 
 // ------------------------------------------------------------------ lean wave tile: loads, then compute
 // Global inputs of one wave's tile, held in registers: lean_load issues every HBM read of the tile back to
-// back, lean_compute consumes them.  walker_step_lean_pf keeps the NEXT tile's LeanIn in flight while the
-// current tile computes.
+// back, lean_compute consumes them.
 template <int NE>
 struct LeanIn {
     float p3[3], v3[3];          // this lane's mass: pos, vel (the springs gather them with ds_bpermute)
@@ -1360,25 +1224,6 @@ __device__ __forceinline__ double lane_gather_d(double v, int src_byte) {
                             __builtin_amdgcn_ds_bpermute(src_byte, __double2loint(v)));
 }
 
-// QUO: one end's share of an edge, formed by the edge lane: the spring quotient t/m (float64, Point.forced
-// with a float64 force, gym/engine.py:67,75) and the damping quotient df/m (float32, gym/optimized_walker.py:
-// 105-106), the end's sign already applied to t and df (division is sign-symmetric), stored at the end's
-// slot in its mass's incidence list.  The unguarded Markstein quotients equal the IEEE ones whenever they
-// are finite (mass_step); otherwise the IEEE divisions are redone here (cold).
-__device__ __forceinline__ void end_terms(double t0, double t1, double t2, float f0, float f1, float f2, float mf,
-                                          double ym, double *sq, float *sqd, int slot, int n2) {
-    const double md = (double)mf;
-    const float ymf = (float)ym;
-    double q0 = ddiv_fast(t0, md, ym), q1 = ddiv_fast(t1, md, ym), q2 = ddiv_fast(t2, md, ym);
-    float c0 = fdiv_fast(f0, mf, ymf), c1 = fdiv_fast(f1, mf, ymf), c2 = fdiv_fast(f2, mf, ymf);
-    if (__builtin_expect(!(__builtin_isfinite(q0 + q1 + q2) && __builtin_isfinite(c0 + c1 + c2)), 0)) {
-        q0 = t0 / md; q1 = t1 / md; q2 = t2 / md;
-        c0 = f0 / mf; c1 = f1 / mf; c2 = f2 / mf;
-    }
-    sq[slot] = q0; sq[n2 + slot] = q1; sq[2 * n2 + slot] = q2;
-    sqd[slot] = c0; sqd[n2 + slot] = c1; sqd[2 * n2 + slot] = c2;
-}
-
 // pair_mode bits 1 / 2: Point.gravity / Point.coulomb (gym/engine.py:128-147) restricted to the walker's
 // masses, after its springs.  Mass q meets its partners in the reference pair loop's order
 // (i < j): ascending partner index.  Per partner: r = max(norm(p_i - p_j) as float64, Config.r);
@@ -1455,12 +1300,28 @@ __device__ __forceinline__ void pair_forces(const wg_batch &b, const KParams &kp
     }
 }
 
-// One wave's tile after its loads.  QUO = false: the edge lanes leave the spring term t and the damping
-// force df per edge in LDS, the mass lanes divide by m while walking their incidence lists (mass_step).
-// QUO = true: the edge lanes also form both ends' quotients (end_terms, edge-parallel: 83 % lane use for the
-// canonical walker) and the mass lanes only add them in order (the list walk runs to the wave's longest
-// list, ~2x the mean, so moving the divisions out of it removes most of its cost).  Same bits either way.
-template <bool IN3D, int NE, bool QUO>
+// Spring-term layout of the lean kernels: interleaved (default) or planes (-DWG_LEAN_SOA=1, an A/B build).
+// Measured on the canonical bench (scripts/variant_ab.py, 5 interleaved rounds, one box): interleaved 47.3 us
+// per launch, planes 48.1 — the planes make the edge lanes' stores conflict-free, but the mass loop's random
+// reads then need three separate 8-B reads per term instead of one ds_read2_b64 + one ds_read_b64.
+#ifndef WG_LEAN_SOA
+#define WG_LEAN_SOA 0
+#endif
+#if WG_LEAN_SOA
+typedef TermsSoA LeanTerms;
+__device__ __forceinline__ LeanTerms lean_terms(char *sl, const LeanGeo &lg) {
+    return TermsSoA{reinterpret_cast<double *>(sl), reinterpret_cast<float *>(sl + lg.off_df), lg.pl};
+}
+#else
+typedef TermsAoS LeanTerms;
+__device__ __forceinline__ LeanTerms lean_terms(char *sl, const LeanGeo &lg) {
+    return TermsAoS{reinterpret_cast<double *>(sl), reinterpret_cast<float *>(sl + lg.off_df)};
+}
+#endif
+
+// One wave's tile after its loads: the edge lanes leave the spring term t and the damping force df of every
+// edge in LDS, then each mass lane walks its incidence list, dividing by m as the reference does (mass_step).
+template <bool IN3D, int NE>
 __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &kp, const wg_outputs &o,
                                              const LeanGeo &lg, char *sl, const LeanTile &t, int lane,
                                              const LeanIn<NE> &L) {
@@ -1469,37 +1330,18 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
     const int wl = t.wl, q = t.q, mu_wl = t.mu_wl, mu_ua = t.mu_ua;
     const bool is_mass = t.is_mass, is_mus = t.is_mus, acts = t.acts;
     const uint32_t pl = t.P0 + lane, ul = t.U0 + lane;   // this lane's mass / muscle
-    // slice: QUO = false: t (f64 x3 per edge) | df (f32 x3) | incidence words | muscle x
-    //        QUO = true:  q (f64, 3 planes of n2 slots) | df/m (f32, 3 planes) | slot of each (edge, end) | x
-    // the obs tile aliases the first region once the masses are done
-    double *s_t = reinterpret_cast<double *>(sl);
-    float *s_df = reinterpret_cast<float *>(sl + lg.off_df);
+    // slice: spring terms t (f64 x3) | df (f32 x3) | incidence words | muscle x; the obs tile aliases the spring
+    // terms once the masses are done
+    const LeanTerms ts = lean_terms(sl, lg);
     uint32_t *s_inc = reinterpret_cast<uint32_t *>(sl + lg.off_inc);
-    uint16_t *s_slot = reinterpret_cast<uint16_t *>(sl + lg.off_inc);
     float *s_x = reinterpret_cast<float *>(sl + lg.off_x);
     const float mf = L.mf;
     const bool pin = L.pin != 0;
-    STAMP(0);
 
     // ================= incidence lists into LDS; act (gym/optimized_walker.py:27-43,164-172)
-    if (QUO) {
-        // incidence word le holds entries 2le, 2le+1 of the tile's list, both of walker le / K: record for each
-        // (edge << 1 | end) its position in its mass's list, the slot its quotients go to
 #pragma unroll
-        for (int it = 0; it < NE; it++) {
-            const int le = lane + 64 * it;
-            if (le < nE) {
-                const int base = 2 * K * fdiv(le, K, lg.invK);
-                const uint32_t w = L.gi[it];
-                s_slot[base + (int)(w & 0xffffu)] = (uint16_t)(2 * le - base);
-                s_slot[base + (int)(w >> 16)] = (uint16_t)(2 * le + 1 - base);
-            }
-        }
-    } else {
-#pragma unroll
-        for (int it = 0; it < NE; it++)
-            if (lane + 64 * it < nE) s_inc[lane + 64 * it] = L.gi[it];
-    }
+    for (int it = 0; it < NE; it++)
+        if (lane + 64 * it < nE) s_inc[lane + 64 * it] = L.gi[it];
     float x = L.x;
     if (acts) {
         x = (kp.action_mode == 1) ? ((L.a != 0.f) ? x + L.stp : x - L.stp) : x + L.a;
@@ -1510,7 +1352,6 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
     if (is_mus) s_x[lane] = x;
     const double ym = 1.0 / (double)mf;   // IEEE 1/m of this lane's mass: every /m below is exact from it
     wave_sync();
-    STAMP(1);
 
     // ================= springs: gym/engine.py:78-102 + gym/optimized_walker.py:92-106 =================
 #pragma unroll
@@ -1527,34 +1368,21 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
         const float pjx = lane_gather(L.p3[0], bj), pjy = lane_gather(L.p3[1], bj), pjz = lane_gather(L.p3[2], bj);
         const float vix = lane_gather(L.v3[0], bi), viy = lane_gather(L.v3[1], bi), viz = lane_gather(L.v3[2], bi);
         const float vjx = lane_gather(L.v3[0], bj), vjy = lane_gather(L.v3[1], bj), vjz = lane_gather(L.v3[2], bj);
-        const float xr = (le < nE && ew < A) ? s_x[ewl * A + ew] : e.rest;
-        if (QUO) {
-            const float mi = lane_gather(mf, bi), mj = lane_gather(mf, bj);
-            const double ymi = lane_gather_d(ym, bi), ymj = lane_gather_d(ym, bj);
-            if (le < nE) {
-                double t0, t1, t2;
-                float g0, g1, g2;
-                spring_terms(e, xr, pix, piy, piz, pjx, pjy, pjz, vix, viy, viz, vjx, vjy, vjz, t0, t1, t2, g0, g1,
-                             g2, 0);
-                const int base = 2 * K * ewl;
-                const uint32_t ss = *reinterpret_cast<const uint32_t *>(s_slot + base + 2 * ew);
-                // end i: a += t/m_i, a += -df/m_i; end j: a += -t/m_j, a += df/m_j
-                end_terms(t0, t1, t2, -g0, -g1, -g2, mi, ymi, s_t, s_df, base + (int)(ss & 0xffffu), lg.n2);
-                end_terms(-t0, -t1, -t2, g0, g1, g2, mj, ymj, s_t, s_df, base + (int)(ss >> 16), lg.n2);
-            }
-        } else if (le < nE) {
+        // the muscle's rest length read unconditionally (clamped index), then selected by value: a select
+        // between the LDS slot and e.rest became a pointer select (flat load from a stack copy of e)
+        const bool mus = le < nE && ew < A;
+        const float xs = s_x[mus ? ewl * A + ew : 0];
+        const float xr = mus ? xs : e.rest;
+        if (le < nE) {
             if (WG_ABLATE & 1) {   // profiling builds only: no spring arithmetic
-                s_t[3 * le] = xr + pix + pjx + vix + vjx; s_t[3 * le + 1] = piy + pjy + viy + vjy;
-                s_t[3 * le + 2] = piz + pjz + viz + vjz;
-                s_df[3 * le] = e.k; s_df[3 * le + 1] = e.c; s_df[3 * le + 2] = 0.f;
+                ts.put(le, xr + pix + pjx + vix + vjx, piy + pjy + viy + vjy, piz + pjz + viz + vjz, e.k, e.c, 0.f);
             } else {
-                spring_edge_regs(e, le, xr, pix, piy, piz, pjx, pjy, pjz, vix, viy, viz, vjx, vjy, vjz, s_t, s_df,
+                spring_edge_regs(e, le, xr, pix, piy, piz, pjx, pjy, pjz, vix, viy, viz, vjx, vjy, vjz, ts,
                                  0);   // lean path: spring_mode 0 only
             }
         }
     }
     wave_sync();
-    STAMP(2);
 
     // ================= masses: ordered accumulation, env forces, Point.run1 =================
     float px = 0.f, py = 0.f, pz = 0.f, vx = 0.f, vy = 0.f, vz = 0.f, ax = 0.f, ay = 0.f, az = 0.f;
@@ -1562,21 +1390,8 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
     bool hit = false;
     if (is_mass) {
         const int r1 = (WG_ABLATE & 2) ? min(L.io1, L.io0 + 1) : L.io1;
-        if (QUO) {
-            // the reference's order: per incident edge (edge order), a = f32(f64(a) + t/m), then a += df/m
-            const int base = 2 * K * wl, n2 = lg.n2;
-            for (int r = L.io0; r < r1; r++) {
-                const int s = base + r;
-                ax = (float)((double)ax + s_t[s]);
-                ay = (float)((double)ay + s_t[n2 + s]);
-                az = (float)((double)az + s_t[2 * n2 + s]);
-                ax = ax + s_df[s]; ay = ay + s_df[n2 + s]; az = az + s_df[2 * n2 + s];
-            }
-        } else {
-            const int lb = wl * K;
-            mass_accumulate(s_t, s_df, reinterpret_cast<const uint16_t *>(s_inc) + 2 * lb, lb, L.io0, r1, mf, ax, ay,
-                            az, 0);
-        }
+        const int lb = wl * K;
+        mass_accumulate(ts, reinterpret_cast<const uint16_t *>(s_inc) + 2 * lb, lb, L.io0, r1, mf, ax, ay, az, 0);
     }
     if (kp.pair_mode) pair_forces(b, kp, L.p3, mf, pl, lane, M, is_mass, ax, ay, az);   // every lane (gathers)
     if (is_mass) {
@@ -1586,7 +1401,6 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
         ke = mf * (nv * nv);   // numpy's float32 ** 2 is libm powf: may differ by 1 ulp
         pe = (float)((double)mf * kp.g) * (py - kp.ground);
     }
-    STAMP(8);
 
     // ================= per-walker reductions (wave shuffles) + outputs (gym/optimized_env.py:189-248)
     const int gbase = lane & ~(M - 1);
@@ -1599,7 +1413,6 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
     const unsigned long long sb = __ballot(is_mass && nv < 0.1f);
     // M | 64 is a power of two: x / M == x * (1/M) exactly (the same real number, rounded once)
     const float midx = sx * lg.invM, midy = sy * lg.invM, midz = sz * lg.invM;
-    STAMP(9);
     if (is_mass) {
         float *gpo = b.pos + 3 * (size_t)pl, *gvo = b.vel + 3 * (size_t)pl, *gao = b.acc + 3 * (size_t)pl;
         gpo[0] = px; gpo[1] = py; gpo[2] = pz;
@@ -1625,13 +1438,12 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
             if (o.energy) o.energy[wg] = 0.5f * ksum + psum;
         }
     }
-    STAMP(3);
 
     // ================= observation rows: Creature.getstat (gym/optimized_walker.py:129-162) =========
     if (o.obs && !(WG_ABLATE & 16)) {
         constexpr int d = IN3D ? 3 : 2, per = 3 * d;
         const int stride = o.obs_stride, nmid = kp.conmid ? 3 : 0;
-        float *otile = reinterpret_cast<float *>(s_t);
+        float *otile = reinterpret_cast<float *>(sl);
         wave_sync();                      // every lane is done reading the spring terms
         if (is_mass) {
             float *row = otile + wl * stride + per * q;
@@ -1655,7 +1467,6 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
         }
         if (is_mus) otile[mu_wl * stride + per * M + nmid + mu_ua] = x * kp.mk;
         wave_sync();
-        STAMP(5);
         float *ob = o.obs + (uint32_t)w0 * (uint32_t)stride;
         const int n = nw * stride;
         if (((((uintptr_t)ob) & 15) == 0) && (n & 3) == 0) {
@@ -1666,82 +1477,278 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
             for (int i = lane; i < n; i += 64) ob[i] = otile[i];
         }
     }
-    STAMP(6);
 }
 
-// One wave's tile: walkers [tile*wpw, tile*wpw + wpw) of the batch, LDS slice `sl`.
-template <bool IN3D, int NE, bool QUO>
-__device__ __forceinline__ void lean_tile(const wg_batch &b, const KParams &kp, const float *__restrict__ action,
-                                          int action_cols, int action_stride, const wg_outputs &o, const LeanGeo &lg,
-                                          char *sl, int tile, int lane) {
+// NE spring passes per wave need up to 8 x 16-B records in registers: 6 waves per SIMD hold up to NE 4 without
+// spills, NE 8 (up to 512 springs per 64 lanes) gets the 4-wave register budget.
+constexpr int lean_waves(int NE) { return NE >= 8 ? 4 : 6; }
+
+// One tile (64 / M walkers) per wave; waves never wait for one another.
+template <bool IN3D, int NE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lean_waves(NE)))) void walker_step_lean(
+    wg_batch b, KParams kp, const float *__restrict__ action, int action_cols, int action_stride, wg_outputs o,
+    LeanGeo lg) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int tile = blockIdx.x * lg.wpb + wv;
+    if (tile * lg.wpw >= b.N) return;
     const LeanTile t = lean_tile_of(b, action, action_cols, lg, tile, lane);
     LeanIn<NE> L;
-    if (kp.prio == 1) __builtin_amdgcn_s_setprio(2);
+    // load-phase wave priority: this wave's HBM requests leave before other waves' arithmetic
+    if (kp.prio) __builtin_amdgcn_s_setprio(2);
     lean_load<NE>(b, kp, action, action_stride, t, lane, L);
-    if (kp.prio == 1) __builtin_amdgcn_s_setprio(0);
-    if (kp.prio == 2) __builtin_amdgcn_s_setprio(2);
-    lean_compute<IN3D, NE, QUO>(b, kp, o, lg, sl, t, lane, L);
+    if (kp.prio) __builtin_amdgcn_s_setprio(0);
+    lean_compute<IN3D, NE>(b, kp, o, lg, smem + wv * lg.slice, t, lane, L);
 }
 
-// QUO's slice (~12 KB per wave for the canonical walker) holds a CU to ~3 waves per SIMD, so its register
-// budget is the 3-wave one (no spills) instead of the 6-wave one of the default path.  Eight edge passes
-// (NE 8: up to 512 springs per 64 lanes) and the persistent form's prefetch registers do not fit the
-// 6-wave budget either: 4 / 5 waves keep them spill-free (their LDS slices bound occupancy near there).
-constexpr int lean_waves(int NE, bool PERSIST, bool QUO) {
-    return QUO ? 3 : NE >= 8 ? 4 : PERSIST ? 5 : 6;
-}
-template <bool IN3D, int NE, bool PERSIST, bool QUO>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lean_waves(NE, PERSIST, QUO)))) void walker_step_lean(
-    wg_batch b, KParams kp, const float *__restrict__ action, int action_cols, int action_stride, wg_outputs o,
-    LeanGeo lg) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    char *sl = smem + wv * lg.slice;
-    int tile = blockIdx.x * lg.wpb + wv;
-    if (!PERSIST) {
-        if (tile * lg.wpw < b.N)
-            lean_tile<IN3D, NE, QUO>(b, kp, action, action_cols, action_stride, o, lg, sl, tile, lane);
-        return;
+// ------------------------------------------------------------------ ragged wave kernel
+// Mixed-topology batches whose walkers all have M_w <= 64 (wg_batch.ragged = 2).  The host sorts the walkers by
+// size and packs them into wave tiles (wg_plan_waves): contiguous stored walkers with at most 64 masses, 64
+// muscles, RW_MAXW walkers and 64 * NE springs in all.  One wave per tile and no workgroup barrier, with the lean
+// kernel's arithmetic: one mass per lane (the tile's walkers side by side), the springs in NE passes of 64 lanes
+// with the endpoints' state gathered by ds_bpermute, each mass lane walking its incidence list in reference
+// order.  What differs from the uniform lean kernel is bookkeeping: a lane finds its walker by a binary search
+// over the tile's walker offsets in LDS; per-walker reductions run 8 lanes per walker over an LDS copy of the
+// per-mass terms in numpy's orders (as walker_step_kernel); observation rows are assembled in LDS and streamed to
+// the caller's rows (wg_batch.row), zero padded to the stride.
+constexpr int RW_MAXW = 32;   // walkers per wave tile (planner cap)
+
+struct RagGeo {
+    int wpb;                  // waves per workgroup
+    int slice;                // LDS bytes per wave
+    int off_df, off_inc, off_x, off_wo, off_terms, off_red;   // byte offsets in the slice (spring terms at 0)
+};
+
+__device__ __forceinline__ int wave_locate(const int *off, int n, int x) {   // largest w < n with off[w] <= x
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (off[mid] <= x) lo = mid; else hi = mid - 1;
     }
-    // persistent grid: a wave's tiles are tile, tile + (waves in the grid), ...
-    const int stride = gridDim.x * lg.wpb;
-    for (; tile * lg.wpw < b.N; tile += stride) {
-        int t_opaque = tile, l_opaque = lane;
-        asm volatile("" : "+v"(l_opaque), "+v"(t_opaque));   // keep per-tile index math inside the loop
-        lean_tile<IN3D, NE, QUO>(b, kp, action, action_cols, action_stride, o, lg, sl, t_opaque, l_opaque);
-        wave_sync();                                          // the next tile reuses the slice
-    }
+    return lo;
 }
 
-// Persistent waves with a one-tile register prefetch: while tile t computes, the loads of tile t + (waves in
-// the grid) are already in flight in a second LeanIn, so each wave hides its own HBM latency behind its own
-// compute instead of relying on other resident waves (the extra registers cost occupancy: 3 waves / SIMD).
-template <bool IN3D, int NE, bool QUO>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void walker_step_lean_pf(
+template <bool IN3D, int NE>
+// LDS (~8.3 KB per wave at NE 2) holds a CU to ~4-5 waves per SIMD: the 5-wave register budget costs nothing
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4 : 5))) void walker_step_waves(
     wg_batch b, KParams kp, const float *__restrict__ action, int action_cols, int action_stride, wg_outputs o,
-    LeanGeo lg) {
+    const int32_t *__restrict__ plan, int ntiles, RagGeo rg) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    char *sl = smem + wv * lg.slice;
-    const int ntiles = (b.N + lg.wpw - 1) / lg.wpw;
-    const int stride = gridDim.x * lg.wpb;
-    int tile = blockIdx.x * lg.wpb + wv;
+    const int tile = blockIdx.x * rg.wpb + wv;
     if (tile >= ntiles) return;
-    LeanIn<NE> nxt;
-    lean_load<NE>(b, kp, action, action_stride, lean_tile_of(b, action, action_cols, lg, tile, lane), lane, nxt);
-    for (; tile < ntiles; tile += stride) {
-        const LeanIn<NE> cur = nxt;
-        if (tile + stride < ntiles)
-            lean_load<NE>(b, kp, action, action_stride, lean_tile_of(b, action, action_cols, lg, tile + stride, lane),
-                          lane, nxt);
-        lean_compute<IN3D, NE, QUO>(b, kp, o, lg, sl, lean_tile_of(b, action, action_cols, lg, tile, lane), lane, cur);
-        wave_sync();                                          // the next tile reuses the slice
+    char *sl = smem + wv * rg.slice;
+    const TermsAoS ts{reinterpret_cast<double *>(sl), reinterpret_cast<float *>(sl + rg.off_df)};
+    uint32_t *s_inc = reinterpret_cast<uint32_t *>(sl + rg.off_inc);
+    float *s_x = reinterpret_cast<float *>(sl + rg.off_x);
+    int *s_mo = reinterpret_cast<int *>(sl + rg.off_wo);              // [RW_MAXW + 1] tile-local offsets
+    int *s_eo = s_mo + (RW_MAXW + 1), *s_uo = s_eo + (RW_MAXW + 1), *s_row = s_uo + (RW_MAXW + 1);
+    float *s_tp = reinterpret_cast<float *>(sl + rg.off_terms);       // pos [64*3] | |v| | m|v|^2 | m g (y-ground)
+    float *s_tn = s_tp + 192, *s_tk = s_tn + 64, *s_te = s_tk + 64;
+    float *s_red = reinterpret_cast<float *>(sl + rg.off_red);        // [RW_MAXW * 8]
+
+    // ================= loads: the tile's walker offsets first (the lane maps need them), then everything else
+    if (kp.prio) __builtin_amdgcn_s_setprio(2);
+    const int w0 = plan[tile], w1 = plan[tile + 1], nw = w1 - w0;
+    const int P0 = b.mass_off[w0], E0 = b.edge_off[w0], U0 = b.muscle_off[w0];
+    const int nP = b.mass_off[w1] - P0, nE = b.edge_off[w1] - E0, nU = b.muscle_off[w1] - U0;
+    int wmo = 0, weo = 0, wuo = 0, wrow = 0, wsteps = 0;
+    if (lane <= nw) {
+        wmo = b.mass_off[w0 + lane] - P0; weo = b.edge_off[w0 + lane] - E0; wuo = b.muscle_off[w0 + lane] - U0;
+    }
+    if (lane < nw) { wrow = caller_row(b, w0 + lane); wsteps = b.steps[w0 + lane]; }
+    const bool is_mass = lane < nP, is_mus = lane < nU;
+    float p3[3] = {0.f, 0.f, 0.f}, v3[3] = {0.f, 0.f, 0.f};
+    float mf = 0.f;
+    int pin = 0;
+    if (is_mass) {
+        const float *gp = b.pos + 3 * (size_t)(P0 + lane), *gv = b.vel + 3 * (size_t)(P0 + lane);
+        p3[0] = gp[0]; p3[1] = gp[1]; p3[2] = gp[2];
+        v3[0] = gv[0]; v3[1] = gv[1]; v3[2] = gv[2];
+        mf = b.mass[P0 + lane];
+        if (b.pinned) pin = b.pinned[P0 + lane];
+    }
+    EdgeRec er[NE];
+    uint32_t gi[NE];
+    const uint32_t *incw = reinterpret_cast<const uint32_t *>(b.inc) + E0;
+#pragma unroll
+    for (int it = 0; it < NE; it++) {
+        const int le = lane + 64 * it;
+        if (le < nE) { er[it] = load_edge(b.edges, E0 + le); gi[it] = incw[le]; }
+    }
+    float mx = 0.f, mlo = 0.f, mhi = 0.f, mst = 0.f;
+    if (is_mus) {
+        mx = b.muscle_x[U0 + lane];
+        if (action) {
+            const float2 bd = reinterpret_cast<const float2 *>(b.muscle_bounds)[U0 + lane];
+            mlo = bd.x; mhi = bd.y;
+            if (kp.action_mode == 1) mst = b.muscle_stride[U0 + lane];
+        }
+    }
+    // lane -> walker maps (tile-local offsets in LDS)
+    if (lane <= nw) { s_mo[lane] = wmo; s_eo[lane] = weo; s_uo[lane] = wuo; }
+    if (lane < nw) s_row[lane] = wrow;
+    wave_sync();
+    const int mw = is_mass ? wave_locate(s_mo, nw, lane) : 0;            // this lane's mass: walker
+    const int mlm = s_mo[mw], mM = s_mo[mw + 1] - mlm, mlb = s_eo[mw];
+    int io0 = 0, io1 = 0;
+    if (is_mass) {
+        const uint32_t io = (uint32_t)(P0 + lane) + (uint32_t)(w0 + mw);   // inc_off: M_w + 1 per walker
+        io0 = b.inc_off[io]; io1 = b.inc_off[io + 1];
+    }
+    const int uw = is_mus ? wave_locate(s_uo, nw, lane) : 0;             // this lane's muscle: walker
+    const int ua = lane - s_uo[uw];
+    const bool acts = action != nullptr && is_mus && ua < action_cols;
+    float act = 0.f;
+    if (acts) act = action[(size_t)s_row[uw] * action_stride + ua];
+    if (kp.prio) __builtin_amdgcn_s_setprio(0);
+
+    // ================= incidence lists into LDS; act (gym/optimized_walker.py:27-43,164-172)
+#pragma unroll
+    for (int it = 0; it < NE; it++)
+        if (lane + 64 * it < nE) s_inc[lane + 64 * it] = gi[it];
+    float x = mx;
+    if (acts) {
+        x = (kp.action_mode == 1) ? ((act != 0.f) ? x + mst : x - mst) : x + act;
+        if (mlo > x) x = mlo;     // Python max(x, originx*minl)
+        if (mhi < x) x = mhi;     // Python min(x, originx*maxl)
+        b.muscle_x[U0 + lane] = x;
+    }
+    if (is_mus) s_x[lane] = x;
+    const double ym = 1.0 / (double)mf;
+    wave_sync();
+
+    // ================= springs: gym/engine.py:78-102 + gym/optimized_walker.py:92-106 =================
+#pragma unroll
+    for (int it = 0; it < NE; it++) {
+        if (64 * it >= nE) continue;                       // wave-uniform
+        const int le = lane + 64 * it;
+        const EdgeRec e = er[it];
+        const int ew_w = wave_locate(s_eo, nw, min(le, max(nE - 1, 0)));
+        const int elm = s_mo[ew_w], ew = le - s_eo[ew_w], eA = s_uo[ew_w + 1] - s_uo[ew_w];
+        const int bi = (elm + edge_i(e.ij)) << 2, bj = (elm + edge_j(e.ij)) << 2;
+        const float pix = lane_gather(p3[0], bi), piy = lane_gather(p3[1], bi), piz = lane_gather(p3[2], bi);
+        const float pjx = lane_gather(p3[0], bj), pjy = lane_gather(p3[1], bj), pjz = lane_gather(p3[2], bj);
+        const float vix = lane_gather(v3[0], bi), viy = lane_gather(v3[1], bi), viz = lane_gather(v3[2], bi);
+        const float vjx = lane_gather(v3[0], bj), vjy = lane_gather(v3[1], bj), vjz = lane_gather(v3[2], bj);
+        const bool mus = le < nE && ew < eA;
+        const float xs = s_x[mus ? s_uo[ew_w] + ew : 0];
+        const float xr = mus ? xs : e.rest;
+        if (le < nE)
+            spring_edge_regs(e, le, xr, pix, piy, piz, pjx, pjy, pjz, vix, viy, viz, vjx, vjy, vjz, ts, 0);
+    }
+    wave_sync();
+
+    // ================= masses: ordered accumulation, env forces, Point.run1 =================
+    float px = 0.f, py = 0.f, pz = 0.f, vx = 0.f, vy = 0.f, vz = 0.f, ax = 0.f, ay = 0.f, az = 0.f;
+    bool hit = false;
+    if (is_mass) {
+        mass_accumulate(ts, reinterpret_cast<const uint16_t *>(s_inc) + 2 * mlb, mlb, io0, io1, mf, ax, ay, az, 0);
+        mass_tail(kp, mf, (float)ym, p3, v3, px, py, pz, vx, vy, vz, ax, ay, az, hit, pin != 0);
+        const uint32_t pl = (uint32_t)(P0 + lane);
+        float *gpo = b.pos + 3 * (size_t)pl, *gvo = b.vel + 3 * (size_t)pl, *gao = b.acc + 3 * (size_t)pl;
+        gpo[0] = px; gpo[1] = py; gpo[2] = pz;
+        gvo[0] = vx; gvo[1] = vy; gvo[2] = vz;
+        gao[0] = ax; gao[1] = ay; gao[2] = az;
+        if (b.contact) b.contact[pl] = (uint8_t)hit;
+        if (b.radius) b.radius[pl] = hit ? 3.0 : 1.0;   // gym/optimized_env.py:156,175
+        const float nv = np_norm3(vx, vy, vz);
+        s_tp[3 * lane] = px; s_tp[3 * lane + 1] = py; s_tp[3 * lane + 2] = pz;
+        s_tn[lane] = nv;
+        s_tk[lane] = mf * (nv * nv);   // numpy's float32 ** 2 is libm powf: may differ by 1 ulp
+        s_te[lane] = (float)((double)mf * kp.g) * (py - kp.ground);
+    }
+    wave_sync();
+
+    // ================= per-walker reductions, 8 lanes per walker (numpy's summation orders) ==========
+    // r 0-2: sequential sums of pos[:, r] (getstat mid / info centroid); r 3: pairwise y (np.mean);
+    // r 4-6: pairwise |v|, m|v|^2, m*g*(y - ground); r 7: contact count << 1 | all-stopped
+    for (int idx = lane; idx < nw * 8; idx += 64) {
+        const int w = idx >> 3, r = idx & 7;
+        const int lm = s_mo[w], M = s_mo[w + 1] - lm;
+        float v;
+        if (r == 7) {
+            int hits = 0, all = 1;
+            for (int q = 0; q < M; q++) {
+                hits += (s_tp[3 * (lm + q) + 1] - kp.ground < 0.f);
+                all &= (s_tn[lm + q] < 0.1f);
+            }
+            v = __int_as_float((hits << 1) | all);
+        } else if (r < 3) {
+            v = 0.f;
+            for (int q = 0; q < M; q++) v += s_tp[3 * (lm + q) + r];
+        } else {
+            const float *src = r == 3 ? s_tp + 3 * lm + 1 : r == 4 ? s_tn + lm : r == 5 ? s_tk + lm : s_te + lm;
+            v = np_pairwise<0>(src, M, r == 3 ? 3 : 1);
+        }
+        s_red[idx] = v;
+    }
+    wave_sync();
+    if (lane < nw) {
+        const int M = s_mo[lane + 1] - s_mo[lane];
+        const float fM = (float)M;
+        const float *rd = s_red + 8 * lane;
+        const float cy = rd[3] / fM;
+        const int packed = __float_as_int(rd[7]);
+        const int hits = packed >> 1, all = packed & 1;
+        const int steps = wsteps + 1;
+        b.steps[w0 + lane] = steps;
+        if (o.reward) o.reward[wrow] = (cy + (-(rd[4] / fM)) * 0.1f) + (float)(-(double)hits * 0.5);
+        if (o.done) {
+            int done = steps >= kp.max_steps;
+            if (!done && cy < kp.done_y) done = 1;
+            if (!done && steps > 100) done = all;
+            o.done[wrow] = (uint8_t)done;
+        }
+        if (o.centroid) {
+            o.centroid[3 * wrow] = rd[0] / fM; o.centroid[3 * wrow + 1] = rd[1] / fM; o.centroid[3 * wrow + 2] = rd[2] / fM;
+        }
+        if (o.energy) o.energy[wrow] = 0.5f * rd[5] + rd[6];
+    }
+
+    // ================= observation rows: Creature.getstat (gym/optimized_walker.py:129-162) =========
+    // Walker w's row is per*M_w values, the 3 conmid values, A_w muscle lengths, then zeros to the stride; its
+    // first per*M_w + nmid + A_w values are staged at per*mo_w + nmid*w + uo_w in LDS (the spring-term region).
+    if (o.obs) {
+        constexpr int d = IN3D ? 3 : 2, per = 3 * d;
+        const int stride = o.obs_stride, nmid = kp.conmid ? 3 : 0;
+        float *stg = reinterpret_cast<float *>(sl);
+        if (is_mass) {
+            const float *rd = s_red + 8 * mw;
+            const float fM = (float)mM;
+            float *row = stg + per * mlm + nmid * mw + s_uo[mw] + per * (lane - mlm);
+            const float pm[3] = {px, py, pz}, vm[3] = {vx, vy, vz}, am[3] = {ax, ay, az};
+#pragma unroll
+            for (int c = 0; c < d; c++) {
+                const float mid = kp.midform == 2 ? rd[c] : rd[c] / fM;   // G1 getstat: the SUM
+                row[c] = kp.midform ? (pm[c] - mid) * kp.pk : pm[c] * kp.pk;
+                row[d + c] = vm[c] * kp.vk;
+                row[2 * d + c] = am[c] * kp.ak;
+            }
+        }
+        if (lane < nw && nmid) {
+            const int M = s_mo[lane + 1] - s_mo[lane];
+            float *row = stg + per * s_mo[lane + 1] + nmid * lane + s_uo[lane];
+            const float *rd = s_red + 8 * lane;
+            for (int c = 0; c < 3; c++) row[c] = kp.midform == 2 ? rd[c] : kp.midform ? rd[c] / (float)M : 0.f;
+        }
+        if (is_mus) stg[per * s_mo[uw + 1] + nmid * (uw + 1) + s_uo[uw] + ua] = x * kp.mk;
+        wave_sync();
+        // stream out nw rows of `stride` floats to the caller's rows; row w = i / stride by a float reciprocal
+        const float inv = 1.f / (float)stride;
+        for (int i = lane; i < nw * stride; i += 64) {
+            const int w = fdiv(i, stride, inv), c = i - w * stride;
+            const int base = per * s_mo[w] + nmid * w + s_uo[w];
+            const int len = per * (s_mo[w + 1] - s_mo[w]) + nmid + (s_uo[w + 1] - s_uo[w]);
+            o.obs[(size_t)s_row[w] * stride + c] = c < len ? stg[base + c] : 0.f;
+        }
     }
 }
 
-// reset: v += noise (x, y, z if in3d), steps = 0 (PhysicsEnv.reset, gym/optimized_env.py:53-68)
+// reset: v += noise, steps = 0 (PhysicsEnv.reset, gym/optimized_env.py:53-68).  zmode 0: x, y (2D);
+// 1: x, y, z (in3d); 2: every component whose noise is not exactly +0.0 (wg_reset_noise)
 __global__ void walker_reset_kernel(wg_batch b, const float *__restrict__ noise, const uint8_t *__restrict__ mask,
-                                    int in3d) {
+                                    int zmode) {
     const int P = b.ragged ? b.mass_off[b.N] : b.N * b.M;
     for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < P; q += gridDim.x * blockDim.x) {
         int w;
@@ -1754,9 +1761,12 @@ __global__ void walker_reset_kernel(wg_batch b, const float *__restrict__ noise,
         }
         if (mask && !mask[w]) continue;
         if (noise) {
-            b.vel[3 * q] = b.vel[3 * q] + noise[3 * q];
-            b.vel[3 * q + 1] = b.vel[3 * q + 1] + noise[3 * q + 1];
-            if (in3d) b.vel[3 * q + 2] = b.vel[3 * q + 2] + noise[3 * q + 2];
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                const float n = noise[3 * q + c];
+                const bool add = zmode == 2 ? __float_as_uint(n) != 0u : (c < 2 || zmode == 1);
+                if (add) b.vel[3 * q + c] = b.vel[3 * q + c] + n;
+            }
         }
     }
     for (int w = blockIdx.x * blockDim.x + threadIdx.x; w < b.N; w += gridDim.x * blockDim.x)
@@ -1765,6 +1775,7 @@ __global__ void walker_reset_kernel(wg_batch b, const float *__restrict__ noise,
 
 // ------------------------------------------------------------------ host side
 int env_int(const char *name, int dflt);
+int wave_passes(int M, int K);
 
 KParams make_kparams(const wg_params &p) {
     KParams k;
@@ -1793,10 +1804,9 @@ KParams make_kparams(const wg_params &p) {
     k.g3_rest = (float)p.g3_restitution;
     k.g3_fric = (float)p.g3_friction;
     k.g3_ground = p.g3_ground;
+    k.friction_mode = p.friction_mode;
     k.prio = env_int("WG_LEAN_PRIO", 1);
     k.dt2 = (float)(p.dt * p.dt);
-    static const int stagger = [] { const char *e = getenv("WG_STAGGER"); return e ? atoi(e) : 0; }();
-    k.stagger = stagger;
     return k;
 }
 
@@ -1814,25 +1824,28 @@ int validate(const wg_batch *b) {
     if (b->K > 0 && (!b->edges || !b->inc || !b->inc_off)) return fail(WG_EINVAL, "missing edge pointer");
     if (b->M > 32767) return fail(WG_ERANGE, "M=%d exceeds the 15-bit edge endpoint encoding", b->M);
     if (!b->inc_off) return fail(WG_EINVAL, "missing inc_off");
+    if (b->ragged < 0 || b->ragged > 2) return fail(WG_EINVAL, "ragged must be 0, 1 or 2");
     if (b->ragged && (!b->mass_off || !b->edge_off || !b->muscle_off))
         return fail(WG_EINVAL, "ragged batch without offsets");
+    if (!b->ragged && b->row) return fail(WG_EINVAL, "row (a walker permutation) is for ragged batches only");
+    if (b->ragged == 2 && !wave_passes(b->M, b->K))
+        return fail(WG_EINVAL, "ragged = 2 (wave tiles) needs M <= 64 and at most 8 spring passes (M=%d K=%d)", b->M, b->K);
     return 0;
 }
 
-Geo uniform_geo(const wg_batch *b, int obs_stride) {
+Geo uniform_geo(const wg_batch *b, int obs_stride, bool no_lite = false) {
     Geo g{};
     // walkers per workgroup: fill the 256 mass lanes, keep edges within EPL registers per lane,
     // and make sure the grid has >= 512 workgroups when the batch allows it.
     int W = std::max(1, NTHREADS / b->M);
     if (b->K > 0) W = std::max(1, std::min(W, EPL * NTHREADS / std::max(1, b->K)));
     while (W > 1 && (b->N + W - 1) / W < 512) W = std::max(1, W / 2);
-    if (const char *fw = getenv("WG_DEBUG_WALKERS_PER_BLOCK")) W = std::max(1, atoi(fw));   // experiments only
     g.W = W;
     const bool shfl_shape = b->M <= 64 && (64 % b->M) == 0 && !(WG_ABLATE & 64);
     for (;;) {
         g.Pcap = g.W * b->M; g.Ecap = g.W * b->K; g.Ucap = g.W * b->A;
         g.tbytes = std::max(g.Ecap * 3 * 8, g.W * std::max(0, obs_stride) * 4);
-        g.lite = (shfl_shape && g.W * b->M <= MAXT) ? 1 : 0;
+        g.lite = (shfl_shape && g.W * b->M <= MAXT && !no_lite) ? 1 : 0;   // pair passes need the LDS copies
         g.threads = std::min(MAXT, std::max(64, ((g.W * b->M + 63) / 64) * 64));
         if (b->K > 0 && g.W * b->K > EPL * g.threads) g.threads = MAXT;
         g.lds = carve_bytes(g);
@@ -1863,8 +1876,7 @@ template <bool STEP, bool RAGGED, bool IN3D, int PWD, bool SHFL>
 int launch(const wg_batch *b, const KParams &kp, const float *action, int cols, int astride,
            const wg_outputs &o, const int32_t *plan, int blocks, const Geo &g, hipStream_t stream) {
     if (g.lds > LDS_LIMIT) return fail(WG_ERANGE, "workgroup needs %d B of LDS (> 160 KiB)", g.lds);
-    static const int lds_extra = [] { const char *e = getenv("WG_DEBUG_LDS_EXTRA"); return e ? atoi(e) : 0; }();  // experiments only
-    hipLaunchKernelGGL((walker_step_kernel<STEP, RAGGED, IN3D, PWD, SHFL>), dim3(blocks), dim3(g.threads), g.lds + lds_extra, stream,
+    hipLaunchKernelGGL((walker_step_kernel<STEP, RAGGED, IN3D, PWD, SHFL>), dim3(blocks), dim3(g.threads), g.lds, stream,
                        *b, kp, action, cols, astride, o, plan, g);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(WG_EHIP, "launch failed: %s", hipGetErrorString(e));
@@ -1888,77 +1900,10 @@ int dispatch2(const wg_batch *b, const KParams &kp, bool in3d, const float *a, i
     return in3d ? launch<STEP, false, true, PWD, false>(b, kp, a, cols, astride, o, plan, blocks, g, st)
                 : launch<STEP, false, false, PWD, false>(b, kp, a, cols, astride, o, plan, blocks, g, st);
 }
-// register (shuffle) reductions: every walker's masses are adjacent lanes of one wave
-// Kernel selection for uniform register-reduction batches (diagnostics / A-B runs):
-//   default / WG_STREAM=0 -> walker_step_kernel (staged loads); WG_STREAM=1 -> walker_step_stream one tile per
-//   workgroup; WG_STREAM=2 -> walker_step_stream persistent with next-tile prefetch.
-int stream_mode() {
-    static const int m = [] { const char *e = getenv("WG_STREAM"); return e && *e ? atoi(e) : 0; }();
-    return m;
-}
-bool stream_disabled() { return stream_mode() == 0; }
-bool stream_persist() { return stream_mode() == 2; }
-
-bool stream_ok(const wg_batch *b, const Geo &g) {
-    return !b->ragged && g.lite && (g.W * b->M) % 4 == 0 && (g.W * b->K) % 4 == 0 && b->N % g.W == 0 &&
-           g.W * b->K <= 4 * g.threads && !(WG_ABLATE & 128) && !stream_disabled();
-}
-
-int stream_blocks(const Geo &g) {
-    static thread_local int cus = 0, dev_cached = -1;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-    if (dev != dev_cached) {
-        dev_cached = dev;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
-    }
-    // resident workgroups per CU: LDS share and a 16-wave budget (VGPR-bound kernel, 4 waves / SIMD)
-    const int by_lds = std::max(1, (160 * 1024) / std::max(g.lds, 1));
-    const int by_waves = std::max(1, 16 / std::max(1, g.threads / 64));
-    return std::min(by_lds, by_waves) * std::max(cus, 1);
-}
-
-int launch_stream(const wg_batch *b, const KParams &kp, bool in3d, const float *a, int cols, int astride,
-                  const wg_outputs &o, const Geo &g, hipStream_t st) {
-    Geo gs = g;
-    gs.stage = 1;
-    gs.lds = carve_bytes(gs);
-    if (gs.lds > LDS_LIMIT) return fail(WG_ERANGE, "workgroup needs %d B of LDS (> 160 KiB)", gs.lds);
-    const int ntiles = b->N / g.W;
-    const bool persist = stream_persist();
-    const int grid = persist ? std::max(1, std::min(ntiles, stream_blocks(gs))) : ntiles;
-    const int ne = (g.W * b->K + g.threads - 1) / g.threads;
-#define WG_LAUNCH_STREAM(D3, NE_)                                                                            \
-    do {                                                                                                     \
-        if (persist)                                                                                         \
-            hipLaunchKernelGGL((walker_step_stream<D3, NE_, true>), dim3(grid), dim3(gs.threads), gs.lds, st, \
-                               *b, kp, a, cols, astride, o, gs, ntiles);                                     \
-        else                                                                                                 \
-            hipLaunchKernelGGL((walker_step_stream<D3, NE_, false>), dim3(grid), dim3(gs.threads), gs.lds, st, \
-                               *b, kp, a, cols, astride, o, gs, ntiles);                                     \
-    } while (0)
-    if (in3d) {
-        if (ne <= 1) WG_LAUNCH_STREAM(true, 1); else if (ne == 2) WG_LAUNCH_STREAM(true, 2);
-        else if (ne == 3) WG_LAUNCH_STREAM(true, 3); else WG_LAUNCH_STREAM(true, 4);
-    } else {
-        if (ne <= 1) WG_LAUNCH_STREAM(false, 1); else if (ne == 2) WG_LAUNCH_STREAM(false, 2);
-        else if (ne == 3) WG_LAUNCH_STREAM(false, 3); else WG_LAUNCH_STREAM(false, 4);
-    }
-#undef WG_LAUNCH_STREAM
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return fail(WG_EHIP, "launch failed: %s", hipGetErrorString(e));
-    return 0;
-}
-
 // ---- lean kernel selection: uniform batch, M | 64 with M >= 4, the wave's edges in <= 8 register
 // passes, its muscles in one pass, and a workgroup LDS footprint that keeps >= 2 workgroups per CU.
 // Knobs (read on every call, so one process can A/B them): WG_LEAN=0 selects the barrier kernels;
-// WG_LEAN_PERSIST 0/1/2 (one tile per wave / persistent / persistent + prefetch); WG_LEAN_QUO 0/1 (end
-// quotients in the edge phase); WG_LEAN_WAVES 1/2/4 waves per workgroup; WG_LEAN_PER_CU, WG_LEAN_BLOCKS
-// (persistent grid size: experiments and tests).
-constexpr int LEAN_PERSIST_DEFAULT = 0;
-constexpr int LEAN_QUO_DEFAULT = 0;
-
+// WG_LEAN_WAVES 1/2/4 waves per workgroup; WG_LEAN_PRIO 0/1 load-phase priority.
 int env_int(const char *name, int dflt) {
     const char *e = getenv(name);
     return (e && *e) ? atoi(e) : dflt;
@@ -1981,24 +1926,15 @@ bool lean_geo(const wg_batch *b, int obs_stride, LeanGeo *out, int spring_mode =
     if ((g.wpw * b->K + 63) / 64 > 8 || g.wpw * b->A > 64) return false;
     const int wpb = env_int("WG_LEAN_WAVES", 4);
     g.wpb = (wpb == 1 || wpb == 2) ? wpb : 4;
-    g.persist = std::max(0, std::min(2, env_int("WG_LEAN_PERSIST", LEAN_PERSIST_DEFAULT)));
-    g.n2 = 2 * g.wpw * b->K;
+    const int ew = g.wpw * b->K;                          // springs of a full wave tile
+    g.pl = (ew + 3) & ~3;                                 // plane length: 16-B aligned f64 and f32 planes
     const int obs_b = g.wpw * std::max(0, obs_stride) * 4;
-    for (int quo = (g.persist != 1 && env_int("WG_LEAN_QUO", LEAN_QUO_DEFAULT)) ? 1 : 0; quo >= 0; quo--) {
-        g.quo = quo;
-        if (quo) {   // q (f64 x3 planes) | df/m (f32 x3 planes) | slot per (edge, end) | x
-            g.off_df = align16(std::max(g.n2 * 24, obs_b));
-            g.off_inc = g.off_df + align16(g.n2 * 12);
-            g.off_x = g.off_inc + align16(g.n2 * 2);
-        } else {     // t (f64 x3 per edge) | df (f32 x3) | incidence words | x
-            g.off_df = align16(std::max(g.wpw * b->K * 24, obs_b));
-            g.off_inc = g.off_df + align16(g.wpw * b->K * 12);
-            g.off_x = g.off_inc + align16(g.wpw * b->K * 4);
-        }
-        g.slice = g.off_x + align16(std::max(1, g.wpw * b->A) * 4);
-        if (4 * g.slice <= 80 * 1024) break;
-        if (!quo) return false;
-    }
+    // t (f64 x3) | df (f32 x3) | incidence words | x; the obs tile aliases t
+    g.off_df = align16(std::max(g.pl * 24, obs_b));
+    g.off_inc = g.off_df + align16(g.pl * 12);
+    g.off_x = g.off_inc + align16(ew * 4);
+    g.slice = g.off_x + align16(std::max(1, g.wpw * b->A) * 4);
+    if (4 * g.slice > 80 * 1024) return false;
     g.invK = 1.f / (float)b->K;
     g.invA = 1.f / (float)std::max(1, b->A);
     g.invM = 1.f / (float)M;
@@ -2006,21 +1942,8 @@ bool lean_geo(const wg_batch *b, int obs_stride, LeanGeo *out, int spring_mode =
     return true;
 }
 
-// grid of a lean launch: one tile per wave, or the resident capacity for the persistent variants
-int lean_blocks(const wg_batch *b, const LeanGeo &g) {
-    int blocks = (b->N + g.wpb * g.wpw - 1) / (g.wpb * g.wpw);
-    if (g.persist) {
-        int cus = 256, dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            cus = 256;
-        const int waves_cu = g.persist == 2 ? 12 : 20;   // VGPR-limited waves per CU: 3 / 5 per SIMD (lean_waves)
-        int per_cu = std::max(1, std::min((160 * 1024 - 4096) / (g.wpb * g.slice), waves_cu / g.wpb));
-        per_cu = std::max(1, env_int("WG_LEAN_PER_CU", per_cu));
-        blocks = std::min(blocks, per_cu * cus);
-        blocks = std::min(blocks, std::max(1, env_int("WG_LEAN_BLOCKS", blocks)));   // tests: many tiles per wave
-    }
-    return blocks;
-}
+// grid of a lean launch: one tile (64 / M walkers) per wave
+int lean_blocks(const wg_batch *b, const LeanGeo &g) { return (b->N + g.wpb * g.wpw - 1) / (g.wpb * g.wpw); }
 
 int launch_lean(const wg_batch *b, const KParams &kp, bool in3d, const float *a, int cols, int astride,
                 const wg_outputs &o, const LeanGeo &g, hipStream_t st) {
@@ -2028,23 +1951,8 @@ int launch_lean(const wg_batch *b, const KParams &kp, bool in3d, const float *a,
     const int ne = (g.wpw * b->K + 63) / 64;
     const int lds = g.wpb * g.slice;
 #define WG_LAUNCH_LEAN(D3, NE_)                                                                                  \
-    do {                                                                                                         \
-        if (g.persist == 2 && g.quo)                                                                             \
-            hipLaunchKernelGGL((walker_step_lean_pf<D3, NE_, true>), dim3(blocks), dim3(64 * g.wpb), lds, st, *b, \
-                               kp, a, cols, astride, o, g);                                                      \
-        else if (g.persist == 2)                                                                                 \
-            hipLaunchKernelGGL((walker_step_lean_pf<D3, NE_, false>), dim3(blocks), dim3(64 * g.wpb), lds, st, *b, \
-                               kp, a, cols, astride, o, g);                                                      \
-        else if (g.persist)                                                                                      \
-            hipLaunchKernelGGL((walker_step_lean<D3, NE_, true, false>), dim3(blocks), dim3(64 * g.wpb), lds, st,  \
-                               *b, kp, a, cols, astride, o, g);                                                  \
-        else if (g.quo)                                                                                          \
-            hipLaunchKernelGGL((walker_step_lean<D3, NE_, false, true>), dim3(blocks), dim3(64 * g.wpb), lds, st,  \
-                               *b, kp, a, cols, astride, o, g);                                                  \
-        else                                                                                                     \
-            hipLaunchKernelGGL((walker_step_lean<D3, NE_, false, false>), dim3(blocks), dim3(64 * g.wpb), lds, st, \
-                               *b, kp, a, cols, astride, o, g);                                                  \
-    } while (0)
+    hipLaunchKernelGGL((walker_step_lean<D3, NE_>), dim3(blocks), dim3(64 * g.wpb), lds, st, *b, kp, a, cols,   \
+                       astride, o, g)
 #define WG_LEAN_NE(D3)                                                         \
     do {                                                                       \
         if (ne <= 1) WG_LAUNCH_LEAN(D3, 1);                                    \
@@ -2058,6 +1966,73 @@ int launch_lean(const wg_batch *b, const KParams &kp, bool in3d, const float *a,
 #undef WG_LAUNCH_LEAN
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(WG_EHIP, "launch failed: %s", hipGetErrorString(e));
+    return 0;
+}
+
+// ---- ragged wave kernel (wg_batch.ragged = 2): spring passes, planner, geometry, launch
+// Spring passes of a wave tile from the batch maxima: enough for the longest walker, and for 64 masses of the
+// densest one (K / M springs per mass), rounded up to an instantiated NE (1, 2, 3, 4, 8); 0 = not eligible.
+int wave_passes(int M, int K) {
+    if (M < 1 || M > 64 || K < 0) return 0;
+    int ne = std::max((K + 63) / 64, (K + M - 1) / M);
+    ne = std::max(ne, 1);
+    if (ne > 8) return 0;
+    return ne <= 4 ? ne : 8;
+}
+
+bool rag_geo(const wg_batch *b, int obs_stride, RagGeo *out) {
+    const int ne = wave_passes(b->M, b->K);
+    if (b->ragged != 2 || ne == 0 || b->A > 64) return false;
+    RagGeo g{};
+    const int wpb = env_int("WG_LEAN_WAVES", 4);
+    g.wpb = (wpb == 1 || wpb == 2) ? wpb : 4;
+    const int ec = 64 * ne;                                      // spring slots of a tile
+    const int stage = 4 * (9 * 64 + 3 * RW_MAXW + 64);           // obs staging (aliases the spring terms)
+    (void)obs_stride;
+    g.off_df = align16(std::max(ec * 24, stage));
+    g.off_inc = g.off_df + align16(ec * 12);
+    g.off_x = g.off_inc + align16(ec * 4);
+    g.off_wo = g.off_x + align16(64 * 4);
+    g.off_terms = g.off_wo + align16(4 * (RW_MAXW + 1) * 3 + 4 * RW_MAXW);
+    g.off_red = g.off_terms + align16(4 * 64 * 6);
+    g.slice = g.off_red + align16(4 * RW_MAXW * 8);
+    *out = g;
+    return true;
+}
+
+int launch_waves(const wg_batch *b, const KParams &kp, bool in3d, const float *a, int cols, int astride,
+                 const wg_outputs &o, const int32_t *plan, int ntiles, const RagGeo &g, hipStream_t st) {
+    const int ne = wave_passes(b->M, b->K);
+    const int blocks = (ntiles + g.wpb - 1) / g.wpb;
+    const int lds = g.wpb * g.slice;
+#define WG_LAUNCH_WAVES(D3, NE_)                                                                                  \
+    hipLaunchKernelGGL((walker_step_waves<D3, NE_>), dim3(blocks), dim3(64 * g.wpb), lds, st, *b, kp, a, cols,    \
+                       astride, o, plan, ntiles, g)
+#define WG_WAVES_NE(D3)                                                        \
+    do {                                                                       \
+        if (ne <= 1) WG_LAUNCH_WAVES(D3, 1);                                   \
+        else if (ne == 2) WG_LAUNCH_WAVES(D3, 2);                              \
+        else if (ne == 3) WG_LAUNCH_WAVES(D3, 3);                              \
+        else if (ne == 4) WG_LAUNCH_WAVES(D3, 4);                              \
+        else WG_LAUNCH_WAVES(D3, 8);                                           \
+    } while (0)
+    if (in3d) WG_WAVES_NE(true); else WG_WAVES_NE(false);
+#undef WG_WAVES_NE
+#undef WG_LAUNCH_WAVES
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(WG_EHIP, "launch failed: %s", hipGetErrorString(e));
+    return 0;
+}
+
+int reset_impl(const wg_batch *b, const float *noise, const uint8_t *mask, int zmode, hipStream_t stream) {
+    int rc = validate(b);
+    if (rc) return rc;
+    if (b->N == 0) return 0;
+    const long P = b->ragged ? -1 : (long)b->N * b->M;
+    const int blocks = P > 0 ? (int)std::min<long>((P + 255) / 256, 4096) : 1024;
+    hipLaunchKernelGGL(walker_reset_kernel, dim3(blocks), dim3(256), 0, stream, *b, noise, mask, zmode);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(WG_EHIP, "reset launch failed: %s", hipGetErrorString(e));
     return 0;
 }
 
@@ -2083,18 +2058,20 @@ int run(const wg_batch *b, const wg_params *p, const float *action, int32_t cols
     wg_outputs out = o ? *o : wg_outputs{};
     if (out.obs && out.obs_stride <= 0) return fail(WG_EINVAL, "obs_stride must be > 0");
     const KParams kp = make_kparams(*p);
-    const Geo g = b->ragged ? ragged_geo(b) : uniform_geo(b, out.obs ? out.obs_stride : 0);
+    const Geo g = b->ragged ? ragged_geo(b) : uniform_geo(b, out.obs ? out.obs_stride : 0, step && p->pair_mode != 0);
     if (g.W > g.threads) return fail(WG_ERANGE, "more than %d walkers per workgroup", g.threads);
     const int blocks = b->ragged ? plan_blocks : (b->N + g.W - 1) / g.W;
     LeanGeo lg{};
     const bool use_lean = step && lean_geo(b, out.obs ? out.obs_stride : 0, &lg, p->spring_mode);
+    RagGeo rgeo{};
+    const bool use_waves = step && p->spring_mode == 0 && p->pair_mode == 0 && lean_enabled() &&
+                           rag_geo(b, out.obs ? out.obs_stride : 0, &rgeo);
     if (p->spring_mode < 0 || p->spring_mode > 2)
         return fail(WG_EINVAL, "spring_mode %d: 0 (engine.py), 1 (G2 element), 2 (G3 engine) only", p->spring_mode);
     if (step && (p->pair_mode & ~7))
         return fail(WG_EINVAL, "pair_mode %d: bits 1 (gravity), 2 (coulomb), 4 (bounce) only", p->pair_mode);
-    if (step && p->pair_mode != 0 && !use_lean)
-        return fail(WG_EINVAL, "pair_mode %d needs a uniform batch with M | 64 (4 <= M <= 64), spring_mode 0 "
-                               "(the lean kernel)", p->pair_mode);
+    if (step && p->pair_mode != 0 && p->spring_mode != 0)
+        return fail(WG_EINVAL, "pair_mode %d needs spring_mode 0", p->pair_mode);
     if (step && (p->pair_mode & 4) && !b->radius)
         return fail(WG_EINVAL, "pair_mode 4 (bounce) needs the radius array");
     for (int s = 0; s < n_steps; s++) {
@@ -2110,8 +2087,8 @@ int run(const wg_batch *b, const wg_params *p, const float *action, int32_t cols
             if (rc) return rc;
             continue;
         }
-        if (step && stream_ok(b, g)) {
-            rc = launch_stream(b, kp, p->in3d != 0, a, cols, astride, os, g, stream);
+        if (use_waves) {
+            rc = launch_waves(b, kp, p->in3d != 0, a, cols, astride, os, plan, plan_blocks, rgeo, stream);
             if (rc) return rc;
             continue;
         }
@@ -2142,22 +2119,43 @@ int wg_observe(const wg_batch *b, const wg_params *p, const wg_outputs *o, const
 }
 
 int wg_reset(const wg_batch *b, const wg_params *p, const float *noise, const uint8_t *mask, hipStream_t stream) {
-    int rc = validate(b);
-    if (rc) return rc;
     if (!p) return fail(WG_EINVAL, "null params");
-    if (b->N == 0) return 0;
-    const long P = b->ragged ? -1 : (long)b->N * b->M;
-    const int blocks = P > 0 ? (int)std::min<long>((P + 255) / 256, 4096) : 1024;
-    hipLaunchKernelGGL(walker_reset_kernel, dim3(blocks), dim3(256), 0, stream, *b, noise, mask, p->in3d);
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return fail(WG_EHIP, "reset launch failed: %s", hipGetErrorString(e));
-    return 0;
+    return reset_impl(b, noise, mask, p->in3d ? 1 : 0, stream);
 }
 
 int wg_reset_noise(const wg_batch *b, const float *noise, hipStream_t stream) {
-    wg_params p{};
-    p.in3d = 1;   // every component of noise is added: a 2D caller passes z = 0 (v.z + 0 == v.z)
-    return wg_reset(b, &p, noise, nullptr, stream);
+    // every component except an exact +0.0: a 2D caller's z = +0.0 leaves v.z as it is (-0.0 included)
+    return reset_impl(b, noise, nullptr, 2, stream);
+}
+
+int wg_wave_edge_passes(int32_t M, int32_t K) { return wave_passes(M, K); }
+
+int wg_plan_waves(const int32_t *mass_off, const int32_t *edge_off, const int32_t *muscle_off, int32_t N,
+                  int32_t *plan, int32_t max_tiles) {
+    if (!mass_off || !edge_off || !muscle_off || !plan || N < 0 || max_tiles < 1)
+        return fail(WG_EINVAL, "bad plan args");
+    int Mmax = 1, Kmax = 0;
+    for (int w = 0; w < N; w++) {
+        Mmax = std::max(Mmax, mass_off[w + 1] - mass_off[w]);
+        Kmax = std::max(Kmax, edge_off[w + 1] - edge_off[w]);
+    }
+    const int ne = wave_passes(Mmax, Kmax);
+    if (!ne) return fail(WG_EINVAL, "a walker does not fit one wave (M=%d K=%d)", Mmax, Kmax);
+    int tiles = 0, w = 0;
+    plan[0] = 0;
+    while (w < N) {
+        int P = 0, E = 0, U = 0, n = 0;
+        while (w < N) {
+            const int m = mass_off[w + 1] - mass_off[w], k = edge_off[w + 1] - edge_off[w],
+                      a = muscle_off[w + 1] - muscle_off[w];
+            if (m > 64 || a > 64 || k > 64 * ne) return fail(WG_EINVAL, "walker %d does not fit one wave", w);
+            if (n > 0 && (P + m > 64 || E + k > 64 * ne || U + a > 64 || n + 1 > RW_MAXW)) break;
+            P += m; E += k; U += a; n++; w++;
+        }
+        if (tiles + 1 > max_tiles) return fail(WG_ERANGE, "plan needs more than %d tiles", max_tiles);
+        plan[++tiles] = w;
+    }
+    return tiles;
 }
 
 int wg_plan_ragged(const int32_t *mass_off, const int32_t *edge_off, const int32_t *muscle_off,
@@ -2179,19 +2177,6 @@ int wg_plan_ragged(const int32_t *mass_off, const int32_t *edge_off, const int32
         plan[++blocks] = w;
     }
     return blocks;
-}
-
-// diagnostic builds: copy n block stamp records (8 x u64 each) to host memory; -1 otherwise
-int wg_debug_stamps(unsigned long long *host, int n) {
-#ifdef WG_STAMPS
-    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), (size_t)n * 16 * sizeof(unsigned long long), 0,
-                            hipMemcpyDeviceToHost) != hipSuccess)
-        return WG_EHIP;
-    return 0;
-#else
-    (void)host; (void)n;
-    return WG_EINVAL;
-#endif
 }
 
 int wg_launch_geometry(const wg_batch *b, wg_launch_info *info) {

@@ -61,18 +61,56 @@ class DeviceBatch:
         self.radius = None   # allocated by enable_radius(): the step writes it, so only when bounce needs it
         # placeholders so that zero-size arrays still have a valid device pointer
         self._dummy = torch.zeros(16, dtype=torch.float32, device=dv)
+        # ragged batches are stored sorted by size (layout.pack): row = caller index of each stored walker
+        self.row = _to_dev(host.row, dv) if host.row is not None else None
+        self._perm = {}
+        if host.row is not None:
+            inv = np.empty(self.N, np.int64)
+            inv[host.row] = np.arange(self.N)
+            self._perm = {"walker": torch.from_numpy(inv).to(dv), "row": torch.from_numpy(host.row.astype(np.int64)).to(dv),
+                          "mass": torch.from_numpy(host.mass_perm).to(dv),
+                          "muscle": torch.from_numpy(host.muscle_perm).to(dv)}
         self.plan = None
         self.plan_blocks = 0
+        self.ragged_kind = 0
         if self.ragged:
             L = _lib.load()
             plan = np.zeros(self.N + 1, np.int32)
-            nb = _lib.check(L.wg_plan_ragged(host.mass_off.ctypes.data_as(C.c_void_p),
-                                             host.edge_off.ctypes.data_as(C.c_void_p),
-                                             host.muscle_off.ctypes.data_as(C.c_void_p), self.N,
-                                             plan.ctypes.data_as(C.c_void_p), self.N + 1), "wg_plan_ragged")
+            args = (host.mass_off.ctypes.data_as(C.c_void_p), host.edge_off.ctypes.data_as(C.c_void_p),
+                    host.muscle_off.ctypes.data_as(C.c_void_p), self.N, plan.ctypes.data_as(C.c_void_p), self.N + 1)
+            # wave tiles when every walker fits one wave (the wave kernel), workgroup tiles otherwise
+            if L.wg_wave_edge_passes(self.M, self.K) > 0 and self.A <= 64:
+                nb, self.ragged_kind = _lib.check(L.wg_plan_waves(*args), "wg_plan_waves"), 2
+            else:
+                nb, self.ragged_kind = _lib.check(L.wg_plan_ragged(*args), "wg_plan_ragged"), 1
             self.plan = _to_dev(plan[:nb + 1], dv)
             self.plan_blocks = nb
         self.struct = self._make_struct()
+
+    # ---- the caller's order (ragged batches are stored sorted by size; uniform batches are not permuted)
+    def caller(self, name: str) -> torch.Tensor:
+        """A state tensor in the caller's walker / mass / muscle order: the tensor itself for an unpermuted batch
+        (a live, writable view), a gathered copy for a sorted ragged batch."""
+        t = getattr(self, name)
+        if t is None or not self._perm:
+            return t
+        kind = {"pos": "mass", "vel": "mass", "acc": "mass", "contact": "mass", "radius": "mass",
+                "muscle_x": "muscle", "steps": "walker"}[name]
+        return t.index_select(0, self._perm[kind])
+
+    def stored_mass(self, q: int) -> int:
+        """Stored index of the caller's mass q."""
+        return int(self.host.mass_perm[q]) if self._perm else int(q)
+
+    def to_stored(self, kind: str, t: torch.Tensor) -> torch.Tensor:
+        """A per-mass ('mass') or per-walker ('walker') caller-order tensor in the stored order."""
+        if not self._perm:
+            return t
+        if kind == "walker":
+            return t.index_select(0, self._perm["row"])
+        out = torch.empty_like(t)
+        out.index_copy_(0, self._perm["mass"], t)
+        return out
 
     def enable_radius(self) -> None:
         """Keep Point.r on the device (pair_mode & 4, Point.bounce): the spec's radii or m ** 0.3."""
@@ -91,7 +129,7 @@ class DeviceBatch:
     def _make_struct(self) -> _lib.WgBatch:
         r = self.ragged
         return _lib.WgBatch(
-            N=self.N, M=self.M, K=self.K, A=self.A, ragged=int(r),
+            N=self.N, M=self.M, K=self.K, A=self.A, ragged=self.ragged_kind if r else 0, row=self._p(self.row),
             mass_off=self._p(self.mass_off) if r else None, edge_off=self._p(self.edge_off) if r else None,
             muscle_off=self._p(self.muscle_off) if r else None,
             pos=self._p(self.pos), vel=self._p(self.vel), acc=self._p(self.acc), mass=self._p(self.mass),
@@ -123,7 +161,7 @@ class DeviceBatch:
             muscle_bounds=self._p(self.muscle_bounds) if A == 0 else off(self.muscle_bounds, 2 * A * w0),
             muscle_stride=self._p(self.muscle_stride) if A == 0 else off(self.muscle_stride, A * w0),
             steps=off(self.steps, w0), contact=off(self.contact, M * w0), pinned=off(self.pinned, M * w0),
-            charge=off(self.charge, M * w0), radius=off(self.radius, M * w0))
+            charge=off(self.charge, M * w0), radius=off(self.radius, M * w0), row=None)
 
     def launch_geometry(self) -> dict:
         info = _lib.WgLaunchInfo()

@@ -3,7 +3,8 @@
 Walkers are independent (no inter-walker force on the env path), so a node-wide batch shards into
 contiguous walker blocks, one per rank (one process per GPU, torch.distributed over RCCL/xGMI).
 Stepping needs no communication at all; the only collective is the observation gather at the end
-of a rollout (``gather_rollout``: one all_gather_into_tensor on RCCL, all_gather on gloo).
+of a rollout (``gather_rollout``: one all_gather_into_tensor on RCCL, all_gather on gloo; uneven
+shards are padded to the longest and trimmed).
 Results of shard g are bit-identical to the same walkers stepped on one GPU (tested).
 """
 from __future__ import annotations
@@ -45,12 +46,35 @@ def shard_spec(spec: dict, start: int, stop: int) -> dict:
     return out
 
 
-def gather_rollout(local: torch.Tensor, group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:
-    """Concatenate every rank's [n, ...] block along dim 0 (equal n per rank) — the rollout-end gather."""
+def gather_rollout(local: torch.Tensor, group: Optional[dist.ProcessGroup] = None,
+                   n_total: Optional[int] = None) -> torch.Tensor:
+    """Concatenate every rank's [n_r, ...] block along dim 0, in rank order — the rollout-end gather.
+
+    Blocks may differ in length (shard_bounds gives the first n_total % world ranks one walker more): each
+    block is padded to the longest, gathered with one collective (all_gather_into_tensor on RCCL, all_gather
+    on gloo) and trimmed.  The lengths come from shard_bounds when ``n_total`` is given, otherwise from a
+    small all_gather of every rank's length."""
     world = dist.get_world_size(group)
-    out = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-    if dist.get_backend(group) == "nccl":
-        dist.all_gather_into_tensor(out, local.contiguous(), group=group)
+    rank = dist.get_rank(group)
+    n = int(local.shape[0])
+    if n_total is not None:
+        sizes = [b - a for a, b in (shard_bounds(n_total, world, r) for r in range(world))]
+        if sizes[rank] != n:
+            raise ValueError(f"rank {rank} holds {n} rows, shard_bounds({n_total}, {world}) gives {sizes[rank]}")
     else:
-        dist.all_gather(list(out.chunk(world, 0)), local.contiguous(), group=group)
-    return out
+        t = torch.tensor([n], dtype=torch.int64, device=local.device)
+        all_n = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(all_n, t, group=group)
+        sizes = [int(x.item()) for x in all_n]
+    nmax = max(sizes)
+    block = local.contiguous()
+    if n < nmax:
+        block = torch.cat([block, block.new_zeros((nmax - n,) + tuple(local.shape[1:]))], 0)
+    out = torch.empty((world * nmax,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    if dist.get_backend(group) == "nccl":
+        dist.all_gather_into_tensor(out, block, group=group)
+    else:
+        dist.all_gather(list(out.chunk(world, 0)), block, group=group)
+    if all(sz == nmax for sz in sizes):
+        return out
+    return torch.cat([out[r * nmax:r * nmax + sizes[r]] for r in range(world)], 0)

@@ -51,6 +51,11 @@ class HostLayout:
     pinned: Optional[np.ndarray] = None   # uint8 [P]: DingPoint masses (None = no pinned mass)
     charge: Optional[np.ndarray] = None   # float64 [P]: Point.e (None = Config.e for every point)
     radius: Optional[np.ndarray] = None   # float64 [P]: Point.r (None = m ** 0.3, gym/engine.py:45-46)
+    # ragged batches are stored sorted by size: row [N] = the caller's index of each stored walker, mass_perm /
+    # muscle_perm = the stored index of each caller mass / muscle (None = stored in the caller's order)
+    row: Optional[np.ndarray] = None
+    mass_perm: Optional[np.ndarray] = None
+    muscle_perm: Optional[np.ndarray] = None
     extra: Dict[str, np.ndarray] = field(default_factory=dict)
 
     @property
@@ -66,8 +71,14 @@ class HostLayout:
         return int(self.muscle_off[-1])
 
     def obs_len(self, in3d: bool, conmid: bool) -> np.ndarray:
+        """Observation length of every walker, in the CALLER's order."""
         d = 3 if in3d else 2
-        return (3 * d * np.diff(self.mass_off) + (3 if conmid else 0) + np.diff(self.muscle_off)).astype(np.int32)
+        n = (3 * d * np.diff(self.mass_off) + (3 if conmid else 0) + np.diff(self.muscle_off)).astype(np.int32)
+        if self.row is None:
+            return n
+        out = np.empty_like(n)
+        out[self.row] = n
+        return out
 
 
 def incidence(ei: np.ndarray, ej: np.ndarray, mass_off: np.ndarray, edge_off: np.ndarray):
@@ -112,11 +123,32 @@ def incidence(ei: np.ndarray, ej: np.ndarray, mass_off: np.ndarray, edge_off: np
     return inc, inc_off
 
 
-def pack(spec: Dict[str, np.ndarray], mx: Optional[np.ndarray] = None, steps: Optional[np.ndarray] = None) -> HostLayout:
-    """Pack a flat CSR spec (see walker_gym_amd.synthetic) into the HBM layout."""
+def pack(spec: Dict[str, np.ndarray], mx: Optional[np.ndarray] = None, steps: Optional[np.ndarray] = None,
+         sort: bool = True) -> HostLayout:
+    """Pack a flat CSR spec (see walker_gym_amd.synthetic) into the HBM layout.  A ragged batch is stored sorted
+    by walker size (``sort``; HostLayout.row / mass_perm / muscle_perm map it back to the caller's order)."""
+    if mx is not None:
+        spec = dict(spec, mx=mx)
+    if steps is not None:
+        spec = dict(spec, steps=steps)
+    Ms, Ks = np.diff(np.asarray(spec["mass_off"])), np.diff(np.asarray(spec["edge_off"]))
+    nm = np.asarray(spec["n_muscles"])
+    uniform = len(Ms) > 0 and np.all(Ms == Ms[0]) and np.all(Ks == Ks[0]) and np.all(nm == nm[0])
+    row = mass_perm = muscle_perm = None
+    if sort and not uniform and len(Ms) > 1:
+        order = size_order(spec)
+        if np.any(order != np.arange(len(order))):
+            spec = reorder_walkers(spec, order)
+            if spec.get("steps") is not None:
+                spec["steps"] = np.asarray(spec["steps"])[order]
+            row, mass_perm, muscle_perm = order.astype(np.int32), spec["_mass_perm"], spec["_muscle_perm"]
+    lay = _pack(spec, spec.get("mx"), spec.get("steps"))
+    lay.row, lay.mass_perm, lay.muscle_perm = row, mass_perm, muscle_perm
+    return lay
+
+
+def _pack(spec: Dict[str, np.ndarray], mx: Optional[np.ndarray], steps: Optional[np.ndarray]) -> HostLayout:
     s = {k: np.asarray(spec[k]) for k in SPEC_KEYS}
-    if mx is None:
-        mx = spec.get("mx")
     mass_off = np.ascontiguousarray(s["mass_off"], np.int32)
     edge_off = np.ascontiguousarray(s["edge_off"], np.int32)
     n_mus = np.ascontiguousarray(s["n_muscles"], np.int32)
@@ -196,6 +228,49 @@ def _pinned(spec, P: int):
     if pin.shape[0] != P:
         raise ValueError(f"pinned has {pin.shape[0]} entries for {P} masses")
     return (pin != 0).astype(np.uint8) if pin.any() else None
+
+
+def reorder_walkers(spec: Dict[str, np.ndarray], order: np.ndarray) -> Dict[str, np.ndarray]:
+    """The flat CSR spec with its walkers in ``order`` (stored walker w = spec walker order[w])."""
+    order = np.asarray(order, np.int64)
+    mo, eo = np.asarray(spec["mass_off"], np.int64), np.asarray(spec["edge_off"], np.int64)
+    nm = np.asarray(spec["n_muscles"], np.int64)
+    uo = np.concatenate([[0], np.cumsum(nm)])
+
+    def gather(off):
+        lens = np.diff(off)[order]
+        starts = off[:-1][order]
+        idx = np.repeat(starts - np.concatenate([[0], np.cumsum(lens)[:-1]]), lens) + np.arange(int(lens.sum()))
+        return idx, np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+
+    pidx, new_mo = gather(mo)
+    eidx, new_eo = gather(eo)
+    uidx, _ = gather(uo)
+    out = dict(spec)
+    for k in ("m", "pos", "vel", "acc", "pinned", "charge", "radius"):
+        if spec.get(k) is not None:
+            out[k] = np.asarray(spec[k])[pidx]
+    for k in ("ei", "ej", "rest", "k", "c", "flags"):
+        out[k] = np.asarray(spec[k])[eidx]
+    for k in ("minl", "maxl", "stride", "mx"):
+        if spec.get(k) is not None:
+            out[k] = np.asarray(spec[k])[uidx]
+    out["mass_off"], out["edge_off"] = new_mo, new_eo
+    out["n_muscles"] = nm[order].astype(np.int32)
+    out["_mass_perm"] = np.empty(len(pidx), np.int64)
+    out["_mass_perm"][pidx] = np.arange(len(pidx))       # caller mass -> stored mass
+    out["_muscle_perm"] = np.empty(len(uidx), np.int64)
+    out["_muscle_perm"][uidx] = np.arange(len(uidx))
+    return out
+
+
+def size_order(spec: Dict[str, np.ndarray]) -> np.ndarray:
+    """Walkers sorted by (masses, springs, muscles), stable: equal-size walkers become neighbours, so wave and
+    workgroup tiles pack evenly ("sort by bucket")."""
+    M = np.diff(np.asarray(spec["mass_off"], np.int64))
+    K = np.diff(np.asarray(spec["edge_off"], np.int64))
+    A = np.asarray(spec["n_muscles"], np.int64)
+    return np.lexsort((np.arange(len(M)), A, K, M))
 
 
 def algorithmic_bytes_per_walker_step(M: int, K: int, A: int, obs_floats: int) -> int:

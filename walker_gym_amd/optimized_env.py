@@ -58,15 +58,17 @@ class PhysicsEnv:
     def _host_state(self):
         if self._cache is None:
             b = self._env.batch
-            self._cache = {"pos": b.pos.cpu().numpy(), "v": b.vel.cpu().numpy(), "old_a": b.acc.cpu().numpy()}
+            self._cache = {"pos": b.caller("pos").cpu().numpy(), "v": b.caller("vel").cpu().numpy(),
+                           "old_a": b.caller("acc").cpu().numpy()}
         return self._cache
 
     def _point_state(self, index: int, name: str) -> np.ndarray:
         return self._host_state()[name][index].copy()
 
     def _set_point_state(self, index: int, name: str, value) -> None:
-        t = {"pos": self._env.batch.pos, "v": self._env.batch.vel}[name]
-        t[index] = torch.as_tensor(np.asarray(value, np.float32), device=t.device)
+        b = self._env.batch
+        t = {"pos": b.pos, "v": b.vel}[name]
+        t[b.stored_mass(index)] = torch.as_tensor(np.asarray(value, np.float32), device=t.device)
         self._cache = None
 
     def _sync_params(self):
@@ -95,7 +97,7 @@ class PhysicsEnv:
 
     @property
     def steps(self) -> int:
-        return int(self._env.batch.steps[0].item())
+        return int(self._env.steps[0].item())
 
     def step(self, action: Union[List[float], np.ndarray]) -> Tuple[np.ndarray, np.float32, bool, Dict[str, Any]]:
         """gym/optimized_env.py:70-92: act -> physics -> steps += 1 -> obs, reward, done, info."""

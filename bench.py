@@ -2,23 +2,30 @@
 """Headline benchmark: env-steps/sec of the batched walker stepper (BASELINE.json `metric`).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--walkers 65536] [--workload canonical]
-    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \\
         --master-port P bench.py --gpus N --steps K --warmup W
 
-A step = one env step (act -> springs -> env forces -> run1 -> obs/reward/done/info) over the rank's
-batch, with obs/reward/done/info materialised every step.  The batch is split into 2 contiguous walker
-ranges stepped on 2 HIP streams (BatchedPhysicsEnv.run lanes), one launch per range per step: every walker
-takes every step, and one range's next step fills the GPU while the other's drains.  Inputs (state, topology
-and a distinct U(-1,1) action tensor for every timed step) are resident in HBM before timing starts.
-Weak scaling: each rank owns its own `--walkers` walkers (no data-path collective); at rollout end the
-final observations are gathered with one RCCL all_gather_into_tensor (inside the timed region).
-Rank 0 prints ONE JSON line.
+`--gpus N` without a torch.distributed world starts the N rank processes itself (torch.distributed.run, before
+any GPU call) and exits with their status; inside a world whose size differs from --gpus it exits with 2.
+
+A step = one env step (act -> springs -> env forces -> run1 -> obs/reward/done/info) over the rank's batch,
+with obs/reward/done/info materialised every step.  The batch is split into walker ranges stepped on separate
+HIP streams (BatchedPhysicsEnv.run lanes: 2 for batches of >= 2^19 masses), one launch per range per step:
+every walker takes every step, and one range's next step fills the GPU while the other's drains.  Inputs
+(state, topology and a distinct U(-1,1) action tensor for every timed step) are resident in HBM before timing.
+Weak scaling: each rank owns its own `--walkers` walkers (no data-path collective); at rollout end the final
+observations are gathered with one RCCL all_gather_into_tensor (inside the timed region).
+Rank 0 prints ONE JSON line.  Workloads: canonical (M=16, K=40, A=8; config 3/4),
+balance (Balance-v0; config 2 at --walkers 4096), ragged (M ~ U{4..32}; config 5), chain (performance_demo's
+chain of --chain-points masses with per-walker Point.gravity; §8(f) 3).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -31,60 +38,143 @@ METRIC = "env-steps/sec (whole node) at 65 536 walkers; 1/2/4/8 MI355X scaling"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--walkers", type=int, default=65536, help="walkers per GPU")
-    ap.add_argument("--workload", default="canonical", choices=["canonical", "balance", "ragged"])
+    ap.add_argument("--workload", default="canonical", choices=["canonical", "balance", "ragged", "chain"])
+    ap.add_argument("--chain-points", type=int, default=100, help="masses per chain walker (--workload chain)")
+    ap.add_argument("--lanes", type=int, default=None, help="walker ranges on separate streams (default: auto)")
+    ap.add_argument("--graph", action="store_true", help="time a HIP-graph replay of the K steps (and the direct "
+                                                         "calls beside it)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline samples")
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--no-control", action="store_true", help="skip the single-launch (lanes 1) control timing")
-    return ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true", help="rank plumbing only (no GPU): every rank reports itself")
+    return ap.parse_args(argv)
 
 
-def make_spec(workload: str, n: int, seed: int):
-    from walker_gym_amd.synthetic import canonical_walkers, ragged_walkers
+# ---------------------------------------------------------------- rank launcher
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def ensure_world(args) -> None:
+    """--gpus N with no torch.distributed world: start N ranks under torch.distributed.run (a child process,
+    started before this process touches the GPU) and exit with its status.  A world of another size: exit 2."""
+    world = os.environ.get("WORLD_SIZE")
+    if world is None:
+        if args.gpus > 1:
+            cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+                   "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__),
+                   *sys.argv[1:]]
+            env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+            sys.exit(subprocess.call(cmd, env=env))
+        return
+    if int(world) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the torch.distributed world has {world} ranks", file=sys.stderr)
+        sys.exit(2)
+
+
+def dry_run(args) -> None:
+    """Rank plumbing without a GPU (CPU test of the launcher): gloo barrier, every rank prints itself."""
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+        dist.barrier()
+    print(json.dumps({"dry_run": True, "rank": rank, "world": world, "gpus": args.gpus,
+                      "local_rank": int(os.environ.get("LOCAL_RANK", "0"))}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+# ---------------------------------------------------------------- workloads
+def make_spec(workload: str, n: int, seed: int, chain_points: int = 100):
+    from walker_gym_amd.synthetic import canonical_walkers, chain_walkers, ragged_walkers
     from walker_gym_amd.walker import balance_spec
     if workload == "canonical":
         return canonical_walkers(n, seed=seed), dict(in3d=1)
     if workload == "balance":
         return balance_spec(n), dict(in3d=0)
+    if workload == "chain":
+        return chain_walkers(n, chain_points, seed=seed), dict(in3d=1, g=0.0, ground=-1.0e6, pair_mode=1)
     return ragged_walkers(n, seed=seed, mmin=4, mmax=32), dict(in3d=1)
 
 
-def cpu_baseline(spec_fn, params, A, budget_s: float):
-    """The C oracle (oracle/walker_oracle.c, the restated reference loop) on host cores, on a bounded
-    sample of the same workload: single thread, then all usable cores (OpenMP over walkers)."""
+DATA = {"canonical": "synthetic (seeded; SURVEY §8(d) canonical walker M=16, K=40, A=8; U(-1,1) actions, "
+                     "distinct per step)",
+        "balance": "synthetic (Balance-v0 topology, gym/optimized_walker.py:176-199; U(-1,1) actions, distinct per "
+                   "step)",
+        "ragged": "synthetic (seeded mixed topologies, M ~ U{4..32}, K ~ U{M..2M}, A = K // 5; U(-1,1) actions, "
+                  "distinct per step)",
+        "chain": "synthetic (performance_demo chain: U(-100,100) positions, U(-10,10) velocities, Skeleton(k=50) "
+                 "links, per-walker Point.gravity; no muscles)"}
+
+
+def bytes_per_walker_step(host, in3d: bool) -> float:
+    """SURVEY §8(d) algorithmic bytes, averaged over the batch's walkers (each walker's own M, K, A, obs row)."""
+    from walker_gym_amd.layout import algorithmic_bytes_per_walker_step
+    M = np.diff(host.mass_off).astype(np.int64)
+    K = np.diff(host.edge_off).astype(np.int64)
+    A = np.diff(host.muscle_off).astype(np.int64)
+    D = 3 if in3d else 2
+    obs = 3 * D * M + A
+    return float(np.mean(algorithmic_bytes_per_walker_step(M, K, A, obs)))
+
+
+def cpu_baseline(workload, params, chain_points, budget_s: float) -> dict:
+    """The CPU side of the same workload on the box's host cores, on bounded samples:
+    * reference_style: the reference's per-object numpy loop restated (oracle/refstyle.py; bit-exact with the
+      goldens), single process and one spawned process per core, full env step (physics + obs/reward/done/info)
+      and physics alone;
+    * c_port: the C oracle (oracle/walker_oracle.c), single thread and OpenMP over walkers.
+    `value` is reference_style on all cores (the reported baseline), kind "port"."""
     from oracle.oracle import Oracle
-    cores = len(os.sched_getaffinity(0))
-    cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
-    n = 4096
-    spec = spec_fn(n)
-    rng = np.random.default_rng(123)
-    acts = rng.uniform(-1, 1, (8, n, A)).astype(np.float32)
+    from oracle.refstyle import host_cores, throughput
+    cores = host_cores()
+    rs_n = 8 if workload == "chain" else 32
+    spec = make_spec(workload, rs_n, 99, chain_points)[0]
+    A = max(1, int(np.max(spec["n_muscles"])))
+    acts = np.random.default_rng(123).uniform(-1, 1, (8, rs_n, A)).astype(np.float32)
+    share = budget_s / 5
+    rs1 = throughput(spec, params, acts, share)
+    rs1p = throughput(spec, params, acts, share, observe=False)
+    rsn = throughput(spec, params, acts, share, procs=cores)
+    n = 512 if workload == "chain" else 4096
+    spec = make_spec(workload, n, 99, chain_points)[0]
+    acts = np.random.default_rng(123).uniform(-1, 1, (8, n, A)).astype(np.float32)
     res = {}
     for label, thr in (("1", 1), ("all", cores)):
         orc = Oracle(spec, params, n_threads=thr)
         t0 = time.perf_counter(); orc.step(acts[0]); probe = time.perf_counter() - t0
-        share = budget_s * (0.3 if thr == 1 else 0.7)
         steps = int(max(2, min(2000, share / max(probe, 1e-6))))
         t0 = time.perf_counter()
         for s in range(steps):
             orc.step(acts[s % 8])
         dt = time.perf_counter() - t0
-        res[label] = (n * steps / dt, steps, thr)
-    v_all, steps_all, thr_all = res["all"]
-    return {"value": round(v_all, 1), "unit": "env-steps/s", "cores": thr_all, "kind": "port",
-            "sample": f"{n} walkers x {steps_all} steps of the same workload (C oracle restating "
-                      f"gym/engine.py + gym/optimized_env.py), OpenMP over walkers",
-            "value_1core": round(res["1"][0], 1), "sample_1core": f"{n} walkers x {res['1'][1]} steps, 1 thread"}
+        res[label] = (n * steps / dt, steps)
+    return {"value": round(rsn["value"], 1), "unit": "env-steps/s", "cores": rsn["procs"], "kind": "port",
+            "sample": f"{rs_n} walkers of the same workload per process, {rsn['procs']} spawned processes for "
+                      f"{rsn['seconds']:.1f} s: the reference's per-object numpy loop (oracle/refstyle.py), full "
+                      "env step",
+            "reference_style": {"env_step_1core": round(rs1["value"], 1), "physics_only_1core": round(rs1p["value"], 1),
+                                "env_step_all_cores": round(rsn["value"], 1), "procs": rsn["procs"]},
+            "c_port": {"value_1core": round(res["1"][0], 1), "value_all_cores": round(res["all"][0], 1),
+                       "threads": cores, "sample": f"{n} walkers x {res['all'][1]} steps, OpenMP over walkers "
+                                                   "(oracle/walker_oracle.c)"}}
 
 
 def load_traffic(workload: str, walkers: int):
-    """HBM bytes per launch from a committed rocprofv3 PMC run (profiles/*pmc*.json), if present."""
+    """HBM bytes per full-batch launch from a committed rocprofv3 PMC run (profiles/*pmc*.json), if present."""
     import glob
     best = None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), key=os.path.getmtime):   # newest last
@@ -97,12 +187,28 @@ def load_traffic(workload: str, walkers: int):
     return best
 
 
+def timed(env, acts, steps, lanes, stream):
+    """Per-step kernel time with HIP events on `stream` (the calling stream waits for every walker range)."""
+    import torch
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    env.run(acts, steps, lanes=lanes)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / steps
+
+
+# ---------------------------------------------------------------- main
 def main():
     args = parse()
+    ensure_world(args)
+    if args.dry_run:
+        return dry_run(args)
     import torch
     import torch.distributed as dist
     from walker_gym_amd.batched_env import BatchedPhysicsEnv
-    from walker_gym_amd.layout import algorithmic_bytes_per_walker_step, layout_bytes_per_walker_step
+    from walker_gym_amd.distributed import gather_rollout
+    from walker_gym_amd.layout import layout_bytes_per_walker_step
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -121,67 +227,65 @@ def main():
     torch.cuda.set_device(dev)
 
     N = args.walkers
-    spec, params = make_spec(args.workload, N, seed=1000 + rank)
+    spec, params = make_spec(args.workload, N, seed=1000 + rank, chain_points=args.chain_points)
     env = BatchedPhysicsEnv(spec, device=dev, **params)
-    A = env.batch.A
-    M, K = env.batch.M, env.batch.K
+    A = max(1, env.batch.A)
+    lanes = env._lanes(args.lanes)
     gen = torch.Generator(device=dev)
     gen.manual_seed(7 + rank)
     acts_w = (torch.rand((max(args.warmup, 1), N, A), generator=gen, device=dev) * 2 - 1).contiguous()
     acts = (torch.rand((args.steps, N, A), generator=gen, device=dev) * 2 - 1).contiguous()
-    gather_buf = torch.empty((world * N, env.obs_dim), dtype=torch.float32, device=dev) if world > 1 else None
+    stream = torch.cuda.current_stream(dev)
 
-    # warmup (untimed)
+    graph = env.graph(acts, args.steps, lanes=lanes) if args.graph else None
     if args.warmup > 0:
-        env.run(acts_w, args.warmup)
+        env.run(acts_w, args.warmup, lanes=lanes)
+    if graph is not None:
+        graph.replay()                         # warm the graph path too
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    stream = torch.cuda.current_stream(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
-    env.run(acts, args.steps)
+    if graph is not None:
+        graph.replay()
+    else:
+        env.run(acts, args.steps, lanes=lanes)
     ev1.record(stream)
     if world > 1 and not args.no_gather:
-        if backend == "nccl":
-            dist.all_gather_into_tensor(gather_buf, env.obs)  # rollout-end observation gather (RCCL)
-        else:
-            dist.all_gather(list(gather_buf.chunk(world, 0)), env.obs)
+        gather_rollout(env.obs)                # rollout-end observation gather (RCCL all_gather_into_tensor)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    step_ms = ev0.elapsed_time(ev1) / args.steps              # stream-ordered, per launch
+    step_ms = ev0.elapsed_time(ev1) / args.steps
 
     wall_t = torch.tensor([wall], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
     wall_max = float(wall_t.item())
 
-    lanes = env._lanes(None)
-    single_ms = None
-    if rank == 0 and lanes > 1 and not args.no_control:
-        # control: the same kernel as one full-batch launch per step (lanes 1), events on its stream.  This is
-        # the per-dispatch duration a rocprofv3 kernel trace reports (tracing serialises the two streams).
-        n1 = max(20, min(args.steps, 100))
-        env.run(acts[:n1], n1, lanes=1)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        env.run(acts[:n1], n1, lanes=1)
-        e1.record(stream)
-        torch.cuda.synchronize()
-        single_ms = e0.elapsed_time(e1) / n1
-
     if rank == 0:
+        # single-launch control: one full-batch launch per step, HIP events on its stream — the per-dispatch
+        # duration a rocprofv3 kernel trace of `bench.py --lanes 1` reports (profiles/r02_*_kernel_stats*.csv)
+        n1 = max(20, min(args.steps, 200))
+        single_ms = step_ms if (lanes == 1 and graph is None) else None
+        if single_ms is None and not args.no_control:
+            env.run(acts[:n1], n1, lanes=1)
+            single_ms = timed(env, acts[:n1], n1, 1, stream)
+        direct_ms = timed(env, acts, args.steps, lanes, stream) if graph is not None else None
         D = env.obs_dim
-        B = algorithmic_bytes_per_walker_step(M, K, A, D)
-        B_layout = layout_bytes_per_walker_step(M, K, A, D)
-        achieved = B * N / (step_ms * 1e-3) / 1e9
+        B = bytes_per_walker_step(env.batch.host, bool(params.get("in3d")))
+        M, K = env.batch.M, env.batch.K
+        uniform = not env.batch.ragged
+        B_layout = layout_bytes_per_walker_step(M, K, env.batch.A, D) if uniform else None
         tr = load_traffic(args.workload, N)
         geo = env.launch_geometry()
+        head_ms = single_ms if single_ms is not None else step_ms
+        achieved = B * N / (head_ms * 1e-3) / 1e9
         line = {
             "metric": METRIC,
             "value": round(world * N * args.steps / wall_max, 1),
@@ -194,28 +298,43 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (seeded; SURVEY §8(d) canonical walker; U(-1,1) actions, distinct per step)",
-            "config": {"workload": f"{args.workload} walkers, {N} per GPU (M={M}, K={K}, A={A}, obs D={D}), "
-                                   "one fused act+physics+observe launch per env step per walker range "
-                                   f"({env._lanes(None)} ranges on {env._lanes(None)} streams)",
-                       "walkers_per_gpu": N, "total_walkers": world * N, "M": M, "K": K, "A": A, "obs_dim": D,
-                       "parallelism": f"dp{world}", "rollout_gather": world > 1 and not args.no_gather,
-                       "lanes": env._lanes(None), "launch": geo},
+            "data": DATA[args.workload],
+            "config": {"workload": f"{args.workload} walkers, {N} per GPU (M={M}{'' if uniform else ' max'}, "
+                                   f"K={K}{'' if uniform else ' max'}, A={env.batch.A}, obs D={D}), one fused "
+                                   "act+physics+observe launch per env step per walker range "
+                                   f"({lanes} range{'s' if lanes > 1 else ''} on {lanes} stream{'s' if lanes > 1 else ''})"
+                                   + (", replayed as one HIP graph" if graph is not None else ""),
+                       "walkers_per_gpu": N, "total_walkers": world * N, "M": M, "K": K, "A": env.batch.A,
+                       "obs_dim": D, "parallelism": f"dp{world}", "rollout_gather": world > 1 and not args.no_gather,
+                       "lanes": lanes, "launch": geo, "ragged_kind": env.batch.ragged_kind,
+                       **({"chain_points": args.chain_points, "pair_mode": 1} if args.workload == "chain" else {})},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": (tr["hbm_bytes_per_launch"] if tr else None),
-                         "bytes_per_walker_step": B, "layout_bytes_per_walker_step": B_layout,
-                         "kernel_ms_per_step_events": round(step_ms, 5),
-                         "note": (f"achieved = N*B / event time per step; a step is {lanes} concurrent launches "
-                                  "(one per walker range)" if lanes > 1 else "achieved = N*B / event time per launch")},
+                         "bytes_per_walker_step": round(B, 1), "layout_bytes_per_walker_step": B_layout,
+                         "kernel_ms_per_launch": round(head_ms, 5),
+                         "note": "achieved = N * B / the per-launch time of ONE full-batch launch per step (HIP "
+                                 "events on the launching stream; in a rocprofv3 --kernel-trace of this command "
+                                 "these are the full-grid launches, scripts/trace_kernels.py); B = SURVEY §8(d) "
+                                 "algorithmic bytes averaged over the walkers"},
         }
-        if single_ms:
-            a1 = B * N / (single_ms * 1e-3) / 1e9
-            line["roofline"]["single_launch"] = {"lanes": 1, "kernel_ms_per_launch_events": round(single_ms, 5),
-                                                 "achieved": round(a1, 1), "frac": round(a1 / HBM_PEAK_GBS, 4)}
+        if lanes > 1 or graph is not None:
+            a2 = B * N / (step_ms * 1e-3) / 1e9
+            line["roofline"]["concurrent"] = {
+                "lanes": lanes, "kernel_ms_per_step_events": round(step_ms, 5), "achieved": round(a2, 1),
+                "frac": round(a2 / HBM_PEAK_GBS, 4),
+                "note": f"{lanes} walker ranges on {lanes} streams overlap one range's launch tail with the other's "
+                        "next step; a kernel trace serialises the streams, so this figure has events only"}
+        if graph is not None:
+            line["graph"] = {"replay_ms_per_step": round(step_ms, 5), "direct_ms_per_step": round(direct_ms, 5),
+                             "launch_overhead_share": round(max(0.0, 1 - step_ms / direct_ms), 4)}
+        if tr:
+            line["roofline"]["traffic_source"] = tr.get("source")
+        if args.workload == "chain":
+            pairs = N * args.chain_points * (args.chain_points - 1) / 2
+            line["pairs_per_s"] = round(pairs / (head_ms * 1e-3), 1)
         if world == 1 and not args.no_cpu_baseline:
-            fn = lambda n: make_spec(args.workload, n, seed=99)[0]
-            line["cpu_baseline"] = cpu_baseline(fn, params, A, args.cpu_seconds)
+            line["cpu_baseline"] = cpu_baseline(args.workload, params, args.chain_points, args.cpu_seconds)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -23,4 +23,13 @@ if "SQ_WAVE_CYCLES" in out:
 if "FETCH_SIZE" in out and "WRITE_SIZE" in out:
     # gfx950: FETCH_SIZE reads half the bytes of wide coalesced streaming reads (MI355X_MICROARCH.md §HBM)
     print(f"  HBM bytes/launch (2*FETCH + WRITE, KB->B): {(2 * out['FETCH_SIZE'] + out['WRITE_SIZE']) * 1024:.4g}")
-json.dump(out, open(f"gpurun_out/{tag}_summary.json", "w"), indent=1)
+import os
+res = {"workload": os.environ.get("WG_WORKLOAD", "canonical"), "walkers": int(os.environ.get("WG_N", "65536")),
+       "source": f"rocprofv3 --pmc, separate passes over scripts/prof_run.py (one full-batch launch per step), "
+                 f"per-dispatch averages of the step kernel (scripts/gpu_pmc.sh {tag})",
+       "counters": out}
+if "FETCH_SIZE" in out and "WRITE_SIZE" in out:
+    res["hbm_bytes_per_launch"] = round((2 * out["FETCH_SIZE"] + out["WRITE_SIZE"]) * 1024)
+    res["formula"] = ("(2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950: FETCH_SIZE reports half of wide streaming reads; "
+                      "MI355X_MICROARCH.md HBM section)")
+json.dump(res, open(f"gpurun_out/{tag}_summary.json", "w"), indent=1)

@@ -172,3 +172,26 @@ def test_reset_noise_2d_keeps_negative_zero():
     got = env.vel
     assert torch.equal(got.view(torch.int32), ref.view(torch.int32))
     assert (got[:, 2].view(torch.int32) == np.int32(-2 ** 31)).all()   # still -0.0
+
+
+def test_rollout_into_dirty_buffer_zero_pads():
+    """A caller-supplied obs buffer is not assumed clean: the short rows' padding is written as zeros; the env's own
+    (zero-initialised) buffers get only each row's own values (wg_outputs.obs_pad_clean)."""
+    import torch
+    from walker_gym_amd.batched_env import BatchedPhysicsEnv
+    from walker_gym_amd.synthetic import ragged_walkers
+    N, T = 300, 4
+    spec = ragged_walkers(N, seed=12, mmin=3, mmax=30)
+    A = int(np.max(spec["n_muscles"]))
+    acts = np.random.default_rng(12).uniform(-1, 1, (T, N, A)).astype(np.float32)
+    env = BatchedPhysicsEnv(spec, device="cuda:0", in3d=1)
+    sd = env.batch.state_dict()
+    clean, _, _ = env.rollout(acts)
+    env.batch.load_state_dict(sd)
+    dirty = torch.full((T, N, env.obs_dim), 7.0, device="cuda:0")
+    got, _, _ = env.rollout(acts, obs_out=dirty)
+    torch.cuda.synchronize()
+    assert torch.equal(got, clean)
+    lens = env.obs_len
+    for w in range(N):
+        assert (clean[:, w, lens[w]:] == 0).all()

@@ -45,7 +45,8 @@ class WgBatch(C.Structure):
 
 class WgOutputs(C.Structure):
     _fields_ = [("obs", _vp), ("obs_stride", C.c_int32), ("reward", _vp), ("done", _vp),
-                ("centroid", _vp), ("energy", _vp), ("obs_step", C.c_int64), ("out_step", C.c_int64)]
+                ("centroid", _vp), ("energy", _vp), ("obs_step", C.c_int64), ("out_step", C.c_int64),
+                ("obs_pad_clean", C.c_int32)]
 
 
 class WgLaunchInfo(C.Structure):

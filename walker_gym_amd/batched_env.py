@@ -174,10 +174,12 @@ class BatchedPhysicsEnv:
         self.centroid = torch.zeros((N, 3), dtype=torch.float32, device=dv)
         self.energy = torch.zeros(N, dtype=torch.float32, device=dv)
 
-    def _outputs(self, obs=None, reward=None, done=None, centroid=None, energy=None, obs_step=0, out_step=0):
+    def _outputs(self, obs=None, reward=None, done=None, centroid=None, energy=None, obs_step=0, out_step=0,
+                 pad_clean=False):
         p = lambda t: None if t is None else C.c_void_p(t.data_ptr())
         return _lib.WgOutputs(obs=p(obs), obs_stride=self.obs_dim, reward=p(reward), done=p(done),
-                              centroid=p(centroid), energy=p(energy), obs_step=obs_step, out_step=out_step)
+                              centroid=p(centroid), energy=p(energy), obs_step=obs_step, out_step=out_step,
+                              obs_pad_clean=int(pad_clean))
 
     def _stream(self):
         return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
@@ -187,9 +189,10 @@ class BatchedPhysicsEnv:
             if not hasattr(self.params, k):
                 raise AttributeError(k)
             setattr(self.params, k, v)
-        self.obs_len = self.batch.host.obs_len(self.params.in3d, self.params.conmid)
-        if int(self.obs_len.max()) != self.obs_dim:
-            self.obs_dim = int(self.obs_len.max())
+        obs_len = self.batch.host.obs_len(self.params.in3d, self.params.conmid)
+        if not np.array_equal(obs_len, self.obs_len):   # new row lengths: fresh zero-padded outputs
+            self.obs_len = obs_len
+            self.obs_dim = int(obs_len.max())
             self._alloc_outputs()
         if int(self.params.pair_mode) & 4:
             self.batch.enable_radius()
@@ -213,7 +216,7 @@ class BatchedPhysicsEnv:
         """One env step for all walkers: act -> physics -> run1 -> obs/reward/done/info (one launch)."""
         act, cols = self._check_action(action)
         L = _lib.load()
-        o = self._outputs(self.obs, self.reward, self.done, self.centroid, self.energy)
+        o = self._outputs(self.obs, self.reward, self.done, self.centroid, self.energy, pad_clean=True)
         _lib.check(L.wg_step(C.byref(self.batch.struct), C.byref(self._pstruct),
                              None if act is None else C.c_void_p(act.data_ptr()), cols, cols, 0, C.byref(o), 1,
                              None if self.batch.plan is None else C.c_void_p(self.batch.plan.data_ptr()),
@@ -229,7 +232,9 @@ class BatchedPhysicsEnv:
             raise ValueError("actions must be [T, N, A]")
         T, _, cols = actions.shape
         dv = self.device
-        obs_out = torch.empty((T, self.N, self.obs_dim), dtype=torch.float32, device=dv) if obs_out is None else obs_out
+        # zero-filled: a ragged batch's short rows then need only their own values written each step
+        clean = obs_out is None
+        obs_out = torch.zeros((T, self.N, self.obs_dim), dtype=torch.float32, device=dv) if obs_out is None else obs_out
         reward_out = torch.empty((T, self.N), dtype=torch.float32, device=dv) if reward_out is None else reward_out
         done_out = torch.empty((T, self.N), dtype=torch.uint8, device=dv) if done_out is None else done_out
         require_tensor(obs_out, "obs_out", dv, torch.float32, (T, self.N, self.obs_dim))
@@ -239,10 +244,10 @@ class BatchedPhysicsEnv:
         if lanes > 1:
             self._run_lanes(actions, T, lambda w0, w1: self._outputs(
                 obs_out[0, w0:w1], reward_out[0, w0:w1], done_out[0, w0:w1], None, None,
-                obs_step=self.N * self.obs_dim, out_step=self.N), lanes)
+                obs_step=self.N * self.obs_dim, out_step=self.N, pad_clean=clean), lanes)
             return obs_out, reward_out, done_out
         o = self._outputs(obs_out, reward_out, done_out, None, None, obs_step=self.N * self.obs_dim,
-                          out_step=self.N)
+                          out_step=self.N, pad_clean=clean)
         _lib.check(_lib.load().wg_step(
             C.byref(self.batch.struct), C.byref(self._pstruct), C.c_void_p(actions.data_ptr()), cols, cols,
             self.N * cols, C.byref(o), T,
@@ -263,9 +268,9 @@ class BatchedPhysicsEnv:
         if lanes > 1:
             return self._run_lanes(actions, int(n_steps), lambda w0, w1: self._outputs(
                 self.obs[w0:w1], self.reward[w0:w1], self.done[w0:w1], self.centroid[w0:w1] if info else None,
-                self.energy[w0:w1] if info else None), lanes)
+                self.energy[w0:w1] if info else None, pad_clean=True), lanes)
         o = self._outputs(self.obs, self.reward, self.done, self.centroid if info else None,
-                          self.energy if info else None)
+                          self.energy if info else None, pad_clean=True)
         _lib.check(_lib.load().wg_step(
             C.byref(self.batch.struct), C.byref(self._pstruct), C.c_void_p(actions.data_ptr()), cols, cols,
             0 if T == 1 else self.N * cols, C.byref(o), int(n_steps),

@@ -1516,7 +1516,7 @@ constexpr int RW_MAXW = 32;   // walkers per wave tile (planner cap)
 struct RagGeo {
     int wpb;                  // waves per workgroup
     int slice;                // LDS bytes per wave
-    int off_df, off_inc, off_x, off_wo, off_terms, off_red;   // byte offsets in the slice (spring terms at 0)
+    int off_df, off_inc, off_x, off_wo;   // byte offsets in the slice (spring terms at 0)
 };
 
 __device__ __forceinline__ int wave_locate(const int *off, int n, int x) {   // largest w < n with off[w] <= x
@@ -1529,8 +1529,8 @@ __device__ __forceinline__ int wave_locate(const int *off, int n, int x) {   // 
 }
 
 template <bool IN3D, int NE>
-// LDS (~8.3 KB per wave at NE 2) holds a CU to ~4-5 waves per SIMD: the 5-wave register budget costs nothing
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4 : 5))) void walker_step_waves(
+// LDS: ~5.8 KB per wave at NE 2 (27 waves per CU); NE 4 / 8 tiles need more LDS and registers
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4 : NE >= 4 ? 5 : 6))) void walker_step_waves(
     wg_batch b, KParams kp, const float *__restrict__ action, int action_cols, int action_stride, wg_outputs o,
     const int32_t *__restrict__ plan, int ntiles, RagGeo rg) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1543,9 +1543,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
     float *s_x = reinterpret_cast<float *>(sl + rg.off_x);
     int *s_mo = reinterpret_cast<int *>(sl + rg.off_wo);              // [RW_MAXW + 1] tile-local offsets
     int *s_eo = s_mo + (RW_MAXW + 1), *s_uo = s_eo + (RW_MAXW + 1), *s_row = s_uo + (RW_MAXW + 1);
-    float *s_tp = reinterpret_cast<float *>(sl + rg.off_terms);       // pos [64*3] | |v| | m|v|^2 | m g (y-ground)
+    // after the mass loop: per-mass terms in the spring-term region, pos [64*3] | |v| | m|v|^2 | m g (y-ground),
+    // then the obs staging; the walker partials [RW_MAXW * 8] in the damping region
+    float *s_tp = reinterpret_cast<float *>(sl);
     float *s_tn = s_tp + 192, *s_tk = s_tn + 64, *s_te = s_tk + 64;
-    float *s_red = reinterpret_cast<float *>(sl + rg.off_red);        // [RW_MAXW * 8]
+    float *s_red = reinterpret_cast<float *>(sl + rg.off_df);
 
     // ================= loads: the tile's walker offsets first (the lane maps need them), then everything else
     if (kp.prio) __builtin_amdgcn_s_setprio(2);
@@ -1652,6 +1654,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
         gao[0] = ax; gao[1] = ay; gao[2] = az;
         if (b.contact) b.contact[pl] = (uint8_t)hit;
         if (b.radius) b.radius[pl] = hit ? 3.0 : 1.0;   // gym/optimized_env.py:156,175
+    }
+    wave_sync();                       // every lane is done reading the spring terms: their region takes the
+    if (is_mass) {                     // per-mass reduction terms, the damping region the walker partials
         const float nv = np_norm3(vx, vy, vz);
         s_tp[3 * lane] = px; s_tp[3 * lane + 1] = py; s_tp[3 * lane + 2] = pz;
         s_tn[lane] = nv;
@@ -1734,13 +1739,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
         }
         if (is_mus) stg[per * s_mo[uw + 1] + nmid * (uw + 1) + s_uo[uw] + ua] = x * kp.mk;
         wave_sync();
-        // stream out nw rows of `stride` floats to the caller's rows; row w = i / stride by a float reciprocal
-        const float inv = 1.f / (float)stride;
-        for (int i = lane; i < nw * stride; i += 64) {
-            const int w = fdiv(i, stride, inv), c = i - w * stride;
-            const int base = per * s_mo[w] + nmid * w + s_uo[w];
-            const int len = per * (s_mo[w + 1] - s_mo[w]) + nmid + (s_uo[w + 1] - s_uo[w]);
-            o.obs[(size_t)s_row[w] * stride + c] = c < len ? stg[base + c] : 0.f;
+        if (o.obs_pad_clean) {
+            // the rows' padding is already zero: each walker's own values only, one row after the other
+            for (int w = 0; w < nw; w++) {
+                const int base = per * s_mo[w] + nmid * w + s_uo[w];
+                const int len = per * (s_mo[w + 1] - s_mo[w]) + nmid + (s_uo[w + 1] - s_uo[w]);
+                float *dst = o.obs + (size_t)s_row[w] * stride;
+                for (int c = lane; c < len; c += 64) dst[c] = stg[base + c];
+            }
+        } else {
+            // nw whole rows of `stride` floats (zero padded) to the caller's rows; row w = i / stride
+            const float inv = 1.f / (float)stride;
+            for (int i = lane; i < nw * stride; i += 64) {
+                const int w = fdiv(i, stride, inv), c = i - w * stride;
+                const int base = per * s_mo[w] + nmid * w + s_uo[w];
+                const int len = per * (s_mo[w + 1] - s_mo[w]) + nmid + (s_uo[w + 1] - s_uo[w]);
+                o.obs[(size_t)s_row[w] * stride + c] = c < len ? stg[base + c] : 0.f;
+            }
         }
     }
 }
@@ -1989,13 +2004,13 @@ bool rag_geo(const wg_batch *b, int obs_stride, RagGeo *out) {
     const int ec = 64 * ne;                                      // spring slots of a tile
     const int stage = 4 * (9 * 64 + 3 * RW_MAXW + 64);           // obs staging (aliases the spring terms)
     (void)obs_stride;
-    g.off_df = align16(std::max(ec * 24, stage));
-    g.off_inc = g.off_df + align16(ec * 12);
+    // spring terms t (f64 x3), later the per-mass reduction terms, then the obs staging | damping forces df,
+    // later the walker partials | incidence words | muscle x | walker offsets and rows
+    g.off_df = align16(std::max(std::max(ec * 24, stage), 4 * 64 * 6));
+    g.off_inc = g.off_df + align16(std::max(ec * 12, 4 * RW_MAXW * 8));
     g.off_x = g.off_inc + align16(ec * 4);
     g.off_wo = g.off_x + align16(64 * 4);
-    g.off_terms = g.off_wo + align16(4 * (RW_MAXW + 1) * 3 + 4 * RW_MAXW);
-    g.off_red = g.off_terms + align16(4 * 64 * 6);
-    g.slice = g.off_red + align16(4 * RW_MAXW * 8);
+    g.slice = g.off_wo + align16(4 * (RW_MAXW + 1) * 3 + 4 * RW_MAXW);
     *out = g;
     return true;
 }

@@ -123,3 +123,23 @@ def ragged_walkers(N: int, seed: int = 0, mmin: int = 4, mmax: int = 32, string_
         n_muscles=As.astype(np.int32), minl=np.full(U, 0.1, f32), maxl=np.full(U, 1.5, f32),
         stride=np.full(U, 2.0, f32),
     )
+
+
+def chain_walkers(N: int, n_points: int = 100, seed: int = 0):
+    """performance_demo's chain (gym/performance_demo.py:18-47) as N independent walkers: n_points masses of
+    m = 1 at U(-100, 100)^3 with velocities U(-10, 10)^3, linked in order by Skeleton(k=50) springs (rest = the
+    initial distance, damping c = 20, the Skeleton default), no muscles.  The demo steps it with
+    Point.gravity() over the walker's points (pair_mode 1)."""
+    rng = np.random.default_rng(seed)
+    P, K = N * n_points, N * (n_points - 1)
+    pos = rng.uniform(-100, 100, (P, 3)).astype(f32)
+    vel = rng.uniform(-10, 10, (P, 3)).astype(f32)
+    ei = np.tile(np.arange(n_points - 1, dtype=np.int32), N)
+    ej = ei + 1
+    base = np.repeat(np.arange(N) * n_points, n_points - 1)
+    rest = norm3_f32(pos[base + ei] - pos[base + ej]).astype(f32)
+    return dict(m=np.ones(P, f32), pos=pos, vel=vel, acc=np.zeros_like(pos),
+                mass_off=(np.arange(N + 1) * n_points).astype(np.int32), ei=ei, ej=ej.astype(np.int32), rest=rest,
+                k=np.full(K, 50.0, f32), c=np.full(K, 20.0, f32), flags=np.zeros(K, np.uint8),
+                edge_off=(np.arange(N + 1) * (n_points - 1)).astype(np.int32), n_muscles=np.zeros(N, np.int32),
+                minl=np.zeros(0, f32), maxl=np.zeros(0, f32), stride=np.zeros(0, f32))

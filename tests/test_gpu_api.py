@@ -1,0 +1,85 @@
+"""The drop-in API on the GPU against the reference's own env objects (tests/golden/api):
+
+* walker_gym_amd.optimized_env.make_env / PhysicsEnv: np.random.seed -> construction (reset noise) -> seed(s) ->
+  reset() -> step(a) x T returns the same observations (float64 arrays), float32 rewards, done flags (every done
+  branch: max_steps, all-stopped after step 100, the 1,000-step rollout), info dicts and point states as
+  gym/optimized_env.py's PhysicsEnv with the SURVEY §8(c) fixes;
+* walker_gym_amd.env.Environment (G1): random.seed -> construction noise -> step(t) x 50 with varying t gives the
+  states of gym/env.py's Environment, G1 friction included.
+Tolerance: bit-exact everywhere except the energy (numpy's float32 ** 2 is libm powf, the kernel x*x: rtol 1e-6).
+"""
+import glob
+import os
+import random
+
+import numpy as np
+import pytest
+
+from api_replay import g1_creatures
+from conftest import GOLDEN, gpu_available
+
+pytestmark = pytest.mark.gpu
+API = sorted(glob.glob(os.path.join(GOLDEN, "api", "api_*.npz")))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not gpu_available():
+        pytest.skip("no ROCm GPU")
+
+
+@pytest.mark.parametrize("path", API, ids=[os.path.basename(p) for p in API])
+def test_physicsenv_facade_matches_reference(path):
+    from walker_gym_amd.optimized_env import make_env
+    z = np.load(path)
+    np.random.seed(int(z["np_seed_init"]))
+    env = make_env(str(z["env_id"]), in3d=bool(int(z["kwargs_in3d"])), dampk=float(z["kwargs_dampk"]),
+                   rand_sigma=float(z["kwargs_rand_sigma"]), device="cuda:0")
+    env.max_steps = int(z["max_steps"])
+    assert env.seed(int(z["env_seed"])) == [int(z["env_seed"])]
+    obs0 = env.reset()
+    assert isinstance(obs0, np.ndarray) and obs0.dtype == np.float64
+    np.testing.assert_array_equal(obs0, z["out_obs0"])
+    T = z["actions"].shape[0]
+    every = 10 if z["out_pos"].shape[0] != T else 1
+    assert env.get_action_space()["shape"] == (z["actions"].shape[1],)
+    assert env.get_observation_space()["shape"] == (z["out_obs0"].shape[0],)
+    for t in range(T):
+        obs, reward, done, info = env.step(z["actions"][t])
+        assert isinstance(reward, np.float32) and reward == z["out_reward"][t], t
+        assert isinstance(done, bool) and done == bool(z["out_done"][t]), t
+        assert info["steps"] == z["out_steps"][t]
+        assert isinstance(info["total_energy"], np.float32)
+        np.testing.assert_allclose(info["total_energy"], z["out_energy"][t], rtol=1e-6)
+        if (t + 1) % every == 0:
+            s = (t + 1) // every - 1
+            np.testing.assert_array_equal(obs, z["out_obs"][s])
+            assert info["centroid_position"] == list(z["out_centroid"][s])
+            st = env._host_state()
+            np.testing.assert_array_equal(st["pos"], z["out_pos"][s])
+            np.testing.assert_array_equal(st["v"], z["out_vel"][s])
+            np.testing.assert_array_equal(st["old_a"], z["out_acc"][s])
+
+
+def test_g1_environment_facade_matches_reference():
+    from walker_gym_amd.env import Environment
+    z = np.load(os.path.join(GOLDEN, "api", "g1_env.npz"))
+    random.seed(int(z["random_seed"]))
+    env = Environment(g1_creatures(z["g1_names"]), in3d=bool(int(z["in3d"])), dampk=float(z["dampk"]),
+                      randsigma=float(z["randsigma"]), device="cuda:0")
+    np.testing.assert_array_equal(env._host_state()["v"], z["out_vel0"])
+    for s, t in enumerate(z["ts"]):
+        env.step(float(t))
+        st = env._host_state()
+        np.testing.assert_array_equal(st["pos"], z["out_pos"][s])
+        np.testing.assert_array_equal(st["v"], z["out_vel"][s])
+        np.testing.assert_array_equal(st["old_a"], z["out_acc"][s])
+    # the point objects read the device state live (gym/engine.py Point attributes)
+    p = env.creatures[0].phys[0]
+    np.testing.assert_array_equal(p.pos, z["out_pos"][-1][0])
+
+
+def test_make_env_unknown_id_raises():
+    from walker_gym_amd.optimized_env import make_env
+    with pytest.raises(ValueError, match="Unknown environment ID"):
+        make_env("Walker-v9", device="cuda:0")

@@ -71,10 +71,20 @@ class PhysicsEnv:
         t[b.stored_mass(index)] = torch.as_tensor(np.asarray(value, np.float32), device=t.device)
         self._cache = None
 
-    def _sync_params(self):
-        self._env.set_params(g=self.g, dampk=self.dampk, ground=self.ground, groundk=self.ground_k,
-                             grounddamp=self.ground_damp, friction=self.friction, dt=self.time_step,
-                             in3d=bool(self.in3d), max_steps=self.max_steps)
+    _friction_mode = 0   # gym/optimized_env.py:168-172; the G1 Environment (walker_gym_amd.env) uses gym/env.py:41
+
+    def _param_values(self):
+        return dict(g=self.g, dampk=self.dampk, ground=self.ground, groundk=self.ground_k,
+                    grounddamp=self.ground_damp, friction=self.friction, dt=self.time_step, in3d=bool(self.in3d),
+                    max_steps=self.max_steps, friction_mode=self._friction_mode)
+
+    def _sync_params(self, force: bool = True):
+        """Push the env's attributes (the reference keeps them as plain attributes a caller may change between
+        steps, e.g. ``env.max_steps``) to the batched env; without ``force`` only when one of them changed."""
+        vals = self._param_values()
+        if force or vals != getattr(self, "_synced", None):
+            self._env.set_params(**vals)
+            self._synced = vals
 
     @staticmethod
     def _obs_np(obs: torch.Tensor, n: int) -> np.ndarray:
@@ -102,6 +112,7 @@ class PhysicsEnv:
     def step(self, action: Union[List[float], np.ndarray]) -> Tuple[np.ndarray, np.float32, bool, Dict[str, Any]]:
         """gym/optimized_env.py:70-92: act -> physics -> steps += 1 -> obs, reward, done, info."""
         a = np.asarray(action if action is not None else [], dtype=np.float32).reshape(1, -1)
+        self._sync_params(force=False)
         obs, rew, done, info = self._env.step(a if a.shape[1] else None)
         self._cache = None
         c = info["centroid_position"][0].cpu().numpy()
@@ -161,6 +172,6 @@ class Environment(PhysicsEnv):
     def step(self, t):  # type: ignore[override]
         """gym/env.py:48-50: forces, then Point.run1(t)."""
         self.time_step = float(t)
-        self._sync_params()
+        self._sync_params(force=False)
         self._env.step(None)
         self._cache = None

@@ -3,7 +3,9 @@
 
     python scripts/variant_ab.py build NAME=FLAGS ...     # here (CPU): build_ab/lib_NAME.so, e.g.
                                                           #   base= soa0=-DWG_LEAN_SOA=0 abl1=-DWG_ABLATE=1
-    python scripts/variant_ab.py run [rounds] [workload]  # GPU box: every .so in build_ab/, interleaved rounds
+    python scripts/variant_ab.py run [rounds] [workload] [NAME:ENV=V,ENV=V ...]
+                                                          # GPU box: every .so in build_ab/ plus env variants of the
+                                                          # in-tree library, interleaved rounds
 
 Each (variant, round) runs in its own process (WALKER_HIP_LIB picks the library) on the bench workload and
 reports the per-launch time with HIP events for one full-batch launch per step (lanes 1) and for bench.py's
@@ -56,18 +58,22 @@ def time_one(lib, workload, steps=200, warm=20):
     return res
 
 
-def run(rounds, workload):
-    libs = sorted(f for f in os.listdir(OUT) if f.endswith(".so"))
-    allr = {f[4:-3]: [] for f in libs}
+def run(rounds, workload, env_specs=()):
+    variants = [(f[4:-3], os.path.join(OUT, f), {}) for f in sorted(os.listdir(OUT)) if f.endswith(".so")]
+    lib = os.path.join(ROOT, "walker_gym_amd", "libwalker_hip.so")
+    for spec in env_specs:
+        name, _, kv = spec.partition(":")
+        variants.append((name, lib, dict(x.split("=", 1) for x in kv.split(",") if x)))
+    allr = {name: [] for name, _, _ in variants}
     for r in range(rounds):
-        for f in libs:
-            p = subprocess.run([sys.executable, __file__, "one", os.path.join(OUT, f), workload], capture_output=True,
-                               text=True, timeout=300)
+        for name, path, env in variants:
+            p = subprocess.run([sys.executable, __file__, "one", path, workload], capture_output=True,
+                               text=True, timeout=300, env=dict(os.environ, **env))
             if p.returncode:
-                print(f, "FAILED", p.stderr[-400:], flush=True)
+                print(name, "FAILED", p.stderr[-400:], flush=True)
                 raise SystemExit(1)
-            allr[f[4:-3]].append(json.loads(p.stdout.strip().splitlines()[-1]))
-            print(r, f, p.stdout.strip().splitlines()[-1], flush=True)
+            allr[name].append(json.loads(p.stdout.strip().splitlines()[-1]))
+            print(r, name, p.stdout.strip().splitlines()[-1], flush=True)
     summ = {k: {m: round(statistics.median(x[m] for x in v), 2) for m in v[0]} for k, v in allr.items()}
     for k, v in summ.items():
         print(f"{k:16s} " + "  ".join(f"{m} {x:7.2f} us" for m, x in v.items()))
@@ -80,6 +86,7 @@ if __name__ == "__main__":
     if sys.argv[1] == "build":
         build(sys.argv[2:])
     elif sys.argv[1] == "run":
-        run(int(sys.argv[2]) if len(sys.argv) > 2 else 5, sys.argv[3] if len(sys.argv) > 3 else "canonical")
+        run(int(sys.argv[2]) if len(sys.argv) > 2 else 5, sys.argv[3] if len(sys.argv) > 3 else "canonical",
+            sys.argv[4:])
     else:
         print(json.dumps(time_one(sys.argv[2], sys.argv[3])))

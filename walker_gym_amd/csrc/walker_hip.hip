@@ -85,6 +85,20 @@ struct Geo {
     int lite;                  // register-reduction kernels: no LDS for acc, m, reduction terms, offsets
 };
 
+// Diagnostic builds only (-DWG_STAMPS, scripts/stamps.py): lane 0 of every lean wave records s_memtime at its
+// phase boundaries into g_stamps[wave][8] with a vector store; wg_debug_stamps copies them out.  Never in the
+// product build.
+#ifdef WG_STAMPS
+__device__ unsigned long long g_stamps[(1 << 16) * 8];
+#define STAMP(k)                                                                                          \
+    do {                                                                                                  \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                      \
+        if ((threadIdx.x & 63) == 0 && stamp_wave < (1 << 16)) g_stamps[stamp_wave * 8 + (k)] = t_;      \
+    } while (0)
+#else
+#define STAMP(k) do {} while (0)
+#endif
+
 struct Carve {
     double *t;                   // [Ecap*3] spring term RN64(f*dir/dist)
     float *pos, *vel, *acc, *m;  // [Pcap*3] / [Pcap]
@@ -1180,23 +1194,21 @@ __device__ __forceinline__ LeanTile lean_tile_of(const wg_batch &b, const float 
 }
 
 // Every global load of the wave's walkers, issued back to back.
+#ifndef WG_KARG_EARLY
+#define WG_KARG_EARLY 0
+#endif
+// Load order: 0 (default) pos, vel, spring records with their incidence words, mass-loop inputs, muscles;
+// 1 (A/B build) what the springs need first (pos, vel, the muscles' act inputs, the spring records), then what
+// only the mass loop needs, so the wait before the springs leaves the mass-loop loads in flight.  Measured
+// (scripts/variant_ab.py, 5 rounds, one box): 47.7 us per launch for 0, 48.5 for 1 — in steady state a wave
+// spends ~4K of its ~25K cycles on loads and the rest computing (scripts/stamps.py), so there is
+// little latency left to hide.
+#ifndef WG_LOAD_ORDER
+#define WG_LOAD_ORDER 0
+#endif
 template <int NE>
-__device__ __forceinline__ void lean_load(const wg_batch &b, const KParams &kp, const float *__restrict__ action,
-                                          int action_stride, const LeanTile &t, int lane, LeanIn<NE> &L) {
-    const uint32_t pl = t.P0 + lane;        // this lane's mass
-    L.p3[0] = 0.f; L.p3[1] = 0.f; L.p3[2] = 0.f;
-    L.v3[0] = 0.f; L.v3[1] = 0.f; L.v3[2] = 0.f;
-    if (t.is_mass) {
-        const float *gp = b.pos + 3 * (size_t)pl, *gv = b.vel + 3 * (size_t)pl;
-        L.p3[0] = gp[0]; L.p3[1] = gp[1]; L.p3[2] = gp[2];
-        L.v3[0] = gv[0]; L.v3[1] = gv[1]; L.v3[2] = gv[2];
-    }
-    const uint32_t *incw = reinterpret_cast<const uint32_t *>(b.inc) + t.E0;   // 2 u16 entries per word
-#pragma unroll
-    for (int it = 0; it < NE; it++) {
-        const int le = lane + 64 * it;
-        if (le < t.nE) { L.er[it] = load_edge(b.edges, t.E0 + (uint32_t)le); L.gi[it] = incw[(uint32_t)le]; }
-    }
+__device__ __forceinline__ void lean_load_mass(const wg_batch &b, const LeanTile &t, int lane, LeanIn<NE> &L) {
+    const uint32_t pl = t.P0 + lane;
     L.mf = 0.f; L.io0 = 0; L.io1 = 0; L.wsteps = 0; L.pin = 0;
     if (t.is_mass) {
         L.mf = b.mass[pl];
@@ -1205,6 +1217,10 @@ __device__ __forceinline__ void lean_load(const wg_batch &b, const KParams &kp, 
         L.io0 = b.inc_off[io]; L.io1 = b.inc_off[io + 1];
         if (t.q == 0) L.wsteps = b.steps[(uint32_t)(t.w0 + t.wl)];
     }
+}
+template <int NE>
+__device__ __forceinline__ void lean_load_muscles(const wg_batch &b, const KParams &kp, const float *__restrict__ action,
+                                                  int action_stride, const LeanTile &t, int lane, LeanIn<NE> &L) {
     L.x = 0.f; L.lo = 0.f; L.hi = 0.f; L.stp = 0.f; L.a = 0.f;
     const uint32_t ul = t.U0 + lane;        // this lane's muscle
     if (t.is_mus) {
@@ -1216,6 +1232,35 @@ __device__ __forceinline__ void lean_load(const wg_batch &b, const KParams &kp, 
             L.a = action[(uint32_t)(t.w0 + t.mu_wl) * (uint32_t)action_stride + (uint32_t)t.mu_ua];
         }
     }
+}
+template <int NE>
+__device__ __forceinline__ void lean_load(const wg_batch &b, const KParams &kp, const float *__restrict__ action,
+                                          int action_stride, const LeanTile &t, int lane, LeanIn<NE> &L) {
+    const uint32_t pl = t.P0 + lane;        // this lane's mass
+    L.p3[0] = 0.f; L.p3[1] = 0.f; L.p3[2] = 0.f;
+    L.v3[0] = 0.f; L.v3[1] = 0.f; L.v3[2] = 0.f;
+    if (t.is_mass) {
+        const float *gp = b.pos + 3 * (size_t)pl, *gv = b.vel + 3 * (size_t)pl;
+        L.p3[0] = gp[0]; L.p3[1] = gp[1]; L.p3[2] = gp[2];
+        L.v3[0] = gv[0]; L.v3[1] = gv[1]; L.v3[2] = gv[2];
+    }
+    if (WG_LOAD_ORDER) lean_load_muscles<NE>(b, kp, action, action_stride, t, lane, L);
+    const uint32_t *incw = reinterpret_cast<const uint32_t *>(b.inc) + t.E0;   // 2 u16 entries per word
+#pragma unroll
+    for (int it = 0; it < NE; it++) {
+        const int le = lane + 64 * it;
+        if (le < t.nE) L.er[it] = load_edge(b.edges, t.E0 + (uint32_t)le);
+        if (!WG_LOAD_ORDER && le < t.nE) L.gi[it] = incw[(uint32_t)le];
+    }
+    if (WG_LOAD_ORDER) {
+#pragma unroll
+        for (int it = 0; it < NE; it++) {
+            const int le = lane + 64 * it;
+            if (le < t.nE) L.gi[it] = incw[(uint32_t)le];
+        }
+    }
+    lean_load_mass<NE>(b, t, lane, L);
+    if (!WG_LOAD_ORDER) lean_load_muscles<NE>(b, kp, action, action_stride, t, lane, L);
 }
 
 // double gathered from another lane (two ds_bpermute), all lanes taking part
@@ -1333,15 +1378,21 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
     // slice: spring terms t (f64 x3) | df (f32 x3) | incidence words | muscle x; the obs tile aliases the spring
     // terms once the masses are done
     const LeanTerms ts = lean_terms(sl, lg);
+#ifdef WG_STAMPS
+    const int stamp_wave = blockIdx.x * lg.wpb + (threadIdx.x >> 6);
+#endif
     uint32_t *s_inc = reinterpret_cast<uint32_t *>(sl + lg.off_inc);
     float *s_x = reinterpret_cast<float *>(sl + lg.off_x);
     const float mf = L.mf;
     const bool pin = L.pin != 0;
 
-    // ================= incidence lists into LDS; act (gym/optimized_walker.py:27-43,164-172)
+    // ================= act (gym/optimized_walker.py:27-43,164-172); the incidence lists go to LDS after the
+    // springs (WG_LOAD_ORDER 1: their loads are still in flight while the springs run)
+    if (!WG_LOAD_ORDER) {
 #pragma unroll
-    for (int it = 0; it < NE; it++)
-        if (lane + 64 * it < nE) s_inc[lane + 64 * it] = L.gi[it];
+        for (int it = 0; it < NE; it++)
+            if (lane + 64 * it < nE) s_inc[lane + 64 * it] = L.gi[it];
+    }
     float x = L.x;
     if (acts) {
         x = (kp.action_mode == 1) ? ((L.a != 0.f) ? x + L.stp : x - L.stp) : x + L.a;
@@ -1352,6 +1403,7 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
     if (is_mus) s_x[lane] = x;
     const double ym = 1.0 / (double)mf;   // IEEE 1/m of this lane's mass: every /m below is exact from it
     wave_sync();
+    STAMP(2);
 
     // ================= springs: gym/engine.py:78-102 + gym/optimized_walker.py:92-106 =================
 #pragma unroll
@@ -1382,7 +1434,13 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
             }
         }
     }
+    if (WG_LOAD_ORDER) {
+#pragma unroll
+        for (int it = 0; it < NE; it++)
+            if (lane + 64 * it < nE) s_inc[lane + 64 * it] = L.gi[it];
+    }
     wave_sync();
+    STAMP(3);
 
     // ================= masses: ordered accumulation, env forces, Point.run1 =================
     float px = 0.f, py = 0.f, pz = 0.f, vx = 0.f, vy = 0.f, vz = 0.f, ax = 0.f, ay = 0.f, az = 0.f;
@@ -1401,6 +1459,7 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
         ke = mf * (nv * nv);   // numpy's float32 ** 2 is libm powf: may differ by 1 ulp
         pe = (float)((double)mf * kp.g) * (py - kp.ground);
     }
+    STAMP(4);
 
     // ================= per-walker reductions (wave shuffles) + outputs (gym/optimized_env.py:189-248)
     const int gbase = lane & ~(M - 1);
@@ -1439,6 +1498,7 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
         }
     }
 
+    STAMP(5);
     // ================= observation rows: Creature.getstat (gym/optimized_walker.py:129-162) =========
     if (o.obs && !(WG_ABLATE & 16)) {
         constexpr int d = IN3D ? 3 : 2, per = 3 * d;
@@ -1477,6 +1537,14 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
             for (int i = lane; i < n; i += 64) ob[i] = otile[i];
         }
     }
+    STAMP(6);
+#ifdef WG_STAMPS
+    if (lane == 0 && stamp_wave < (1 << 16)) {   // slot 7: HW_ID (gfx9 hwreg 4) | XCC_ID (gfx940+ hwreg 20) << 32
+        const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+        const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+        g_stamps[stamp_wave * 8 + 7] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
+    }
+#endif
 }
 
 // NE spring passes per wave need up to 8 x 16-B records in registers: 6 waves per SIMD hold up to NE 4 without
@@ -1490,14 +1558,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lean_waves(
     LeanGeo lg) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#if WG_KARG_EARLY
+    // experiment: every pointer the tile loads from in SGPRs at entry (one kernarg wait instead of several)
+    asm volatile("" ::"s"(b.pos), "s"(b.vel), "s"(b.edges), "s"(b.inc), "s"(b.inc_off), "s"(b.mass),
+                 "s"(b.muscle_x), "s"(b.muscle_bounds), "s"(b.steps), "s"(action), "s"(b.M), "s"(b.K), "s"(b.A));
+#endif
     const int tile = blockIdx.x * lg.wpb + wv;
     if (tile * lg.wpw >= b.N) return;
+#ifdef WG_STAMPS
+    const int stamp_wave = tile;
+#endif
+    STAMP(0);
     const LeanTile t = lean_tile_of(b, action, action_cols, lg, tile, lane);
     LeanIn<NE> L;
     // load-phase wave priority: this wave's HBM requests leave before other waves' arithmetic
     if (kp.prio) __builtin_amdgcn_s_setprio(2);
     lean_load<NE>(b, kp, action, action_stride, t, lane, L);
     if (kp.prio) __builtin_amdgcn_s_setprio(0);
+    STAMP(1);
     lean_compute<IN3D, NE>(b, kp, o, lg, smem + wv * lg.slice, t, lane, L);
 }
 
@@ -2192,6 +2270,19 @@ int wg_plan_ragged(const int32_t *mass_off, const int32_t *edge_off, const int32
         plan[++blocks] = w;
     }
     return blocks;
+}
+
+// diagnostic builds (-DWG_STAMPS): copy n lean-wave stamp records (8 x u64 each) to host memory; WG_EINVAL otherwise
+int wg_debug_stamps(unsigned long long *host, int n) {
+#ifdef WG_STAMPS
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), (size_t)n * 8 * sizeof(unsigned long long), 0,
+                            hipMemcpyDeviceToHost) != hipSuccess)
+        return fail(WG_EHIP, "stamp copy failed");
+    return 0;
+#else
+    (void)host; (void)n;
+    return fail(WG_EINVAL, "not a stamps build");
+#endif
 }
 
 int wg_launch_geometry(const wg_batch *b, wg_launch_info *info) {

@@ -91,8 +91,10 @@ def dry_run(args) -> None:
     if world > 1:
         dist.init_process_group("gloo")
         dist.barrier()
-    print(json.dumps({"dry_run": True, "rank": rank, "world": world, "gpus": args.gpus,
-                      "local_rank": int(os.environ.get("LOCAL_RANK", "0"))}), flush=True)
+    line = json.dumps({"dry_run": True, "rank": rank, "world": world, "gpus": args.gpus,
+                       "local_rank": int(os.environ.get("LOCAL_RANK", "0"))}) + "\n"
+    sys.stdout.flush()
+    os.write(1, line.encode())   # one write(2) per rank: ranks sharing a pipe cannot interleave inside a line
     if world > 1:
         dist.destroy_process_group()
 

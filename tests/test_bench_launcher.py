@@ -20,8 +20,8 @@ def test_gpus_2_launches_two_ranks():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
                        capture_output=True, text=True, timeout=240, env=_env())
     assert r.returncode == 0, r.stderr[-2000:]
-    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
-    assert sorted(l["rank"] for l in lines) == [0, 1]
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith('{"dry_run"')]
+    assert sorted(l["rank"] for l in lines) == [0, 1], r.stdout[-2000:]
     assert all(l["world"] == 2 and l["gpus"] == 2 for l in lines)
 
 
@@ -29,7 +29,7 @@ def test_single_gpu_needs_no_launcher():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run"], capture_output=True, text=True,
                        timeout=120, env=_env())
     assert r.returncode == 0, r.stderr[-2000:]
-    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith('{"dry_run"')]
     assert len(lines) == 1 and lines[0]["world"] == 1
 
 

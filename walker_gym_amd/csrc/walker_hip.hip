@@ -388,27 +388,50 @@ __device__ __forceinline__ void acc_f64_entry(const IncTerm &q, int ent, double 
 // Env forces on one mass after its spring terms, each one Point.forced in the reference's order: gravity
 // [0,-g,0]/m, damp -dampk*v/m (gym/env.py:32-33, optimized_env.py:148-151), the ground penalty when below
 // ground (:154-172); then Point.run1 / run2 (gym/engine.py:168-190).  a (in: spring terms) becomes old_a.
+// The env forces of one mass in the reference's order, each one Point.forced: a += f/m.  FAST: the unguarded
+// Markstein quotients, exact whenever every quotient is finite — a non-finite one makes the sum non-finite, and
+// the caller then redoes the forces with the guarded ones (fdiv_mk, which equal IEEE division).
+template <bool FAST>
+__device__ __forceinline__ float fdiv_env(float x, float m, float y) { return FAST ? fdiv_fast(x, m, y) : fdiv_mk(x, m, y); }
+template <bool FAST>
+__device__ __forceinline__ void env_forces(const KParams &kp, float mf, float ymf, float vx, float vy, float vz,
+                                           float py, float &ax, float &ay, float &az, bool &hit) {
+    const float zm = fdiv_mk(0.f, mf, ymf);   // the zero components of the env forces, divided by m
+    // gravity [0,-g,0]/m, damp -dampk*v/m  (gym/env.py:32-33, optimized_env.py:148-151)
+    ax = ax + zm; ay = ay + fdiv_env<FAST>(kp.neg_g, mf, ymf); az = az + zm;
+    ax = ax + fdiv_env<FAST>(kp.neg_dampk * vx, mf, ymf);
+    ay = ay + fdiv_env<FAST>(kp.neg_dampk * vy, mf, ymf);
+    az = az + fdiv_env<FAST>(kp.neg_dampk * vz, mf, ymf);
+    const float deep = py - kp.ground;
+    hit = deep < 0.f;                                                // optimized_env.py:154
+    if (hit) {
+        ax = ax + zm; ay = ay + fdiv_env<FAST>(kp.neg_groundk * deep, mf, ymf); az = az + zm;
+        ax = ax + zm; ay = ay + fdiv_env<FAST>(kp.neg_grounddamp * vy, mf, ymf); az = az + zm;
+        const float ff = fabsf(deep) * kp.friction;                  // :168
+        // G1 env (gym/env.py:41): [v_x*deep*friction, 0, v_z*deep*friction], left to right in float32
+        const float fx = kp.friction_mode ? (vx * deep) * kp.friction : (-vx) * ff;
+        const float fz = kp.friction_mode ? (vz * deep) * kp.friction : (-vz) * ff;
+        ax = ax + fdiv_env<FAST>(fx, mf, ymf); ay = ay + zm; az = az + fdiv_env<FAST>(fz, mf, ymf);
+    }
+}
+
+#ifndef WG_FAST_ENV
+#define WG_FAST_ENV 1
+#endif
 __device__ __forceinline__ void mass_tail(const KParams &kp, float mf, float ymf, const float *p3, const float *v3,
                                           float &px, float &py, float &pz, float &vx, float &vy, float &vz,
                                           float &ax, float &ay, float &az, bool &hit, bool pinned) {
     vx = v3[0]; vy = v3[1]; vz = v3[2];
     px = p3[0]; py = p3[1]; pz = p3[2];
-    const float zm = fdiv_mk(0.f, mf, ymf);   // the zero components of the env forces, divided by m
-    // gravity [0,-g,0]/m, damp -dampk*v/m  (gym/env.py:32-33, optimized_env.py:148-151)
-    ax = ax + zm; ay = ay + fdiv_mk(kp.neg_g, mf, ymf); az = az + zm;
-    ax = ax + fdiv_mk(kp.neg_dampk * vx, mf, ymf);
-    ay = ay + fdiv_mk(kp.neg_dampk * vy, mf, ymf);
-    az = az + fdiv_mk(kp.neg_dampk * vz, mf, ymf);
-    const float deep = py - kp.ground;
-    hit = deep < 0.f;                                                // optimized_env.py:154
-    if (hit) {
-        ax = ax + zm; ay = ay + fdiv_mk(kp.neg_groundk * deep, mf, ymf); az = az + zm;
-        ax = ax + zm; ay = ay + fdiv_mk(kp.neg_grounddamp * vy, mf, ymf); az = az + zm;
-        const float ff = fabsf(deep) * kp.friction;                  // :168
-        // G1 env (gym/env.py:41): [v_x*deep*friction, 0, v_z*deep*friction], left to right in float32
-        const float fx = kp.friction_mode ? (vx * deep) * kp.friction : (-vx) * ff;
-        const float fz = kp.friction_mode ? (vz * deep) * kp.friction : (-vz) * ff;
-        ax = ax + fdiv_mk(fx, mf, ymf); ay = ay + zm; az = az + fdiv_mk(fz, mf, ymf);
+    if (WG_FAST_ENV) {
+        const float sx = ax, sy = ay, sz = az;
+        env_forces<true>(kp, mf, ymf, vx, vy, vz, py, ax, ay, az, hit);
+        if (__builtin_expect(!__builtin_isfinite(ax + ay + az), 0)) {   // cold: redo with exact quotients
+            ax = sx; ay = sy; az = sz;
+            env_forces<false>(kp, mf, ymf, vx, vy, vz, py, ax, ay, az, hit);
+        }
+    } else {
+        env_forces<false>(kp, mf, ymf, vx, vy, vz, py, ax, ay, az, hit);
     }
     if (pinned) { ax = 0.f; ay = 0.f; az = 0.f; }   // DingPoint.forced is a no-op: a stays zeros()
     // v += a*t in both integrators; the position update differs.  Both forms are computed and one selected:
@@ -1108,6 +1131,15 @@ __device__ __forceinline__ float lane_gather(float v, int src_byte) {
     return __int_as_float(__builtin_amdgcn_ds_bpermute(src_byte, __float_as_int(v)));
 }
 
+#ifndef WG_FAST_SPRING
+#define WG_FAST_SPRING 1
+#endif
+#ifndef WG_SPRING_PIPE
+#define WG_SPRING_PIPE 0
+#endif
+#ifndef WG_LEAN_WAVES
+#define WG_LEAN_WAVES 6   // waves per SIMD the lean kernel's register budget targets (NE < 8)
+#endif
 // Spring term and damping force of one edge from its endpoints' state (gathered from the mass lanes):
 // spring_edge's arithmetic with the cheaper reciprocal (identical results; cold path unchanged).
 __device__ __forceinline__ void spring_terms(const EdgeRec &e, float x, float pix, float piy, float piz, float pjx,
@@ -1117,8 +1149,14 @@ __device__ __forceinline__ void spring_terms(const EdgeRec &e, float x, float pi
     const float cur = np_norm3(pix - pjx, piy - pjy, piz - pjz);   // engine.py:86
     const float dx = cur - x;                                       // engine.py:96
     const float r0 = pjx - pix, r1 = pjy - piy, r2 = pjz - piz;     // other.pos - self.pos
+#if WG_FAST_SPRING
+    // max(distance, r) as v_max_f64: it differs from Python's max only for a NaN distance, which the cold path
+    // below recomputes (the fast path needs cur >= r anyway)
+    double dist = __builtin_fmax((double)cur, CONFIG_R);
+#else
     double dist = (double)cur;                                      // engine.py:73
     if (CONFIG_R > dist) dist = CONFIG_R;                           // max(distance, r)
+#endif
     const double yc = rcp64_nr(dist);
     const float fsz = (spring_mode == 1 || !(dx < 0.f && edge_string(e.ij))) ? (-dx) * e.k : 0.f;  // :97-100
     const float nf = -fsz;                                                                           // :75
@@ -1131,10 +1169,20 @@ __device__ __forceinline__ void spring_terms(const EdgeRec &e, float x, float pi
         t1 = ddiv_fast((double)(nf * r1), dist, yc);
         t2 = ddiv_fast((double)(nf * r2), dist, yc);
     }
+#if WG_FAST_SPRING
+    // the quotients are exact when the distance is unclamped (cur >= r) and every quotient is finite; a non-finite
+    // one (or NaN distance) makes its sum non-finite (|d| <= 1 cannot overflow a sum of three)
+    const bool fast_ok = (double)cur >= CONFIG_R && __builtin_isfinite(d0 + d1 + d2) && __builtin_isfinite(t0 + t1 + t2);
+#else
     const bool fast_ok = cur > 0.f && (double)cur == dist && __builtin_isfinite(d0) && __builtin_isfinite(d1) &&
                          __builtin_isfinite(d2) && __builtin_isfinite(t0) && __builtin_isfinite(t1) &&
                          __builtin_isfinite(t2);
+#endif
     if (__builtin_expect(!fast_ok, 0)) {
+#if WG_FAST_SPRING
+        dist = (double)cur;
+        if (CONFIG_R > dist) dist = CONFIG_R;                       // Python max(distance, r), NaN kept
+#endif
         d0 = r0; d1 = r1; d2 = r2;
         if (cur > 0.f) { d0 = r0 / cur; d1 = r1 / cur; d2 = r2 / cur; }
         if (spring_mode == 1) {
@@ -1406,20 +1454,25 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
     STAMP(2);
 
     // ================= springs: gym/engine.py:78-102 + gym/optimized_walker.py:92-106 =================
+    // endpoint state from the mass lanes by ds_bpermute: every lane takes part (inactive sources read as 0).
+    // WG_SPRING_PIPE: the gathers of pass it + 1 are issued before the arithmetic of pass it, so their LDS
+    // latency overlaps it (12 more registers).
+    struct Gath { float v[12]; };
+    auto gather = [&](int it, Gath &g) {
+        const int le = lane + 64 * it;
+        const int ewl = fdiv(le, K, lg.invK);
+        const uint32_t ij = L.er[it].ij;
+        const int bi = (ewl * M + edge_i(ij)) << 2, bj = (ewl * M + edge_j(ij)) << 2;
 #pragma unroll
-    for (int it = 0; it < NE; it++) {
-        // a by-value record and no early loop exit: both keep er[] in registers (a reference under a `break`
-        // made hipcc park the rest lengths in scratch right after their loads, serialising them)
-        if (64 * it >= nE) continue;                       // wave-uniform
+        for (int c = 0; c < 3; c++) {
+            g.v[c] = lane_gather(L.p3[c], bi); g.v[3 + c] = lane_gather(L.p3[c], bj);
+            g.v[6 + c] = lane_gather(L.v3[c], bi); g.v[9 + c] = lane_gather(L.v3[c], bj);
+        }
+    };
+    auto spring = [&](int it, const Gath &g) {
         const int le = lane + 64 * it;
         const EdgeRec e = L.er[it];
         const int ewl = fdiv(le, K, lg.invK), ew = le - ewl * K;
-        // endpoint state from the mass lanes: every lane takes part (inactive sources read as 0)
-        const int bi = (ewl * M + edge_i(e.ij)) << 2, bj = (ewl * M + edge_j(e.ij)) << 2;
-        const float pix = lane_gather(L.p3[0], bi), piy = lane_gather(L.p3[1], bi), piz = lane_gather(L.p3[2], bi);
-        const float pjx = lane_gather(L.p3[0], bj), pjy = lane_gather(L.p3[1], bj), pjz = lane_gather(L.p3[2], bj);
-        const float vix = lane_gather(L.v3[0], bi), viy = lane_gather(L.v3[1], bi), viz = lane_gather(L.v3[2], bi);
-        const float vjx = lane_gather(L.v3[0], bj), vjy = lane_gather(L.v3[1], bj), vjz = lane_gather(L.v3[2], bj);
         // the muscle's rest length read unconditionally (clamped index), then selected by value: a select
         // between the LDS slot and e.rest became a pointer select (flat load from a stack copy of e)
         const bool mus = le < nE && ew < A;
@@ -1427,13 +1480,35 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
         const float xr = mus ? xs : e.rest;
         if (le < nE) {
             if (WG_ABLATE & 1) {   // profiling builds only: no spring arithmetic
-                ts.put(le, xr + pix + pjx + vix + vjx, piy + pjy + viy + vjy, piz + pjz + viz + vjz, e.k, e.c, 0.f);
+                ts.put(le, xr + g.v[0] + g.v[3] + g.v[6] + g.v[9], g.v[1] + g.v[4] + g.v[7] + g.v[10],
+                       g.v[2] + g.v[5] + g.v[8] + g.v[11], e.k, e.c, 0.f);
             } else {
-                spring_edge_regs(e, le, xr, pix, piy, piz, pjx, pjy, pjz, vix, viy, viz, vjx, vjy, vjz, ts,
-                                 0);   // lean path: spring_mode 0 only
+                spring_edge_regs(e, le, xr, g.v[0], g.v[1], g.v[2], g.v[3], g.v[4], g.v[5], g.v[6], g.v[7], g.v[8],
+                                 g.v[9], g.v[10], g.v[11], ts, 0);   // lean path: spring_mode 0 only
             }
         }
+    };
+#if WG_SPRING_PIPE
+    Gath g[2];                                             // double buffer: pass it reads g[it & 1]
+    gather(0, g[0]);
+#pragma unroll
+    for (int it = 0; it < NE; it++) {
+        // no early loop exit: it keeps er[] in registers (a reference under a `break` made hipcc park the rest
+        // lengths in scratch right after their loads, serialising them)
+        if (64 * it >= nE) continue;                       // wave-uniform
+        if (it + 1 < NE && 64 * (it + 1) < nE) gather(it + 1, g[(it + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);                 // the next pass's gathers stay above this arithmetic
+        spring(it, g[it & 1]);
     }
+#else
+#pragma unroll
+    for (int it = 0; it < NE; it++) {
+        if (64 * it >= nE) continue;                       // wave-uniform
+        Gath g;
+        gather(it, g);
+        spring(it, g);
+    }
+#endif
     if (WG_LOAD_ORDER) {
 #pragma unroll
         for (int it = 0; it < NE; it++)
@@ -1549,7 +1624,7 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
 
 // NE spring passes per wave need up to 8 x 16-B records in registers: 6 waves per SIMD hold up to NE 4 without
 // spills, NE 8 (up to 512 springs per 64 lanes) gets the 4-wave register budget.
-constexpr int lean_waves(int NE) { return NE >= 8 ? 4 : 6; }
+constexpr int lean_waves(int NE) { return NE >= 8 ? 4 : WG_LEAN_WAVES; }
 
 // One tile (64 / M walkers) per wave; waves never wait for one another.
 template <bool IN3D, int NE>

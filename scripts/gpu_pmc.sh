@@ -1,7 +1,7 @@
 #!/bin/bash
 # PMC passes over scripts/prof_run.py (each pass its own run; counters only, no tracing).
 # usage: [WG_WORKLOAD=ragged] gpu_pmc.sh <tag> [full]  -> gpurun_out/<tag>N/, then scripts/pmc_summary.py <tag>
-# (traffic passes only unless "full" is given)
+# (traffic passes only unless "full" is given; "valu" = the instruction-issue pass only)
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -11,6 +11,7 @@ if [ ! -s gpurun_out/counters_avail.txt ]; then
 fi
 i=0
 sets=("FETCH_SIZE GRBM_GUI_ACTIVE" "WRITE_SIZE SQ_WAVES")
+if [ "$2" = "valu" ]; then sets=("SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_LDS_BANK_CONFLICT" "GRBM_GUI_ACTIVE SQ_WAVES"); fi
 if [ "$2" = "full" ]; then sets+=(\
             "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_LDS_BANK_CONFLICT" \
             "SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS" \

@@ -53,7 +53,7 @@ constexpr int EPL = 4;               // edges per lane per pass held in register
 constexpr int NTHREADS = WG_NTHREADS;   // default workgroup size (walkers fill 256 mass lanes)
 constexpr int MAXT = 256;               // __launch_bounds__: workgroups are 64..256 threads
 #ifndef WG_ABLATE
-#define WG_ABLATE 0   // profiling builds only (scripts/ablate.py): bit k skips phase k; 0 in the product
+#define WG_ABLATE 0   // profiling builds only (scripts/variant_ab.py): bit k skips phase k; 0 in the product
 #endif
 
 // Float32 constants derived from wg_params exactly where numpy rounds the Python scalars.
@@ -375,14 +375,17 @@ __device__ __forceinline__ IncTerm inc_term(const TS &ts, int lb, int ent) { ret
 // p1.forced(-df), p2.forced(df) (optimized_walker.py:105-106); end j sees the opposite signs.
 __device__ __forceinline__ void acc_f64_entry(const IncTerm &q, int ent, double md, double ym, float mf, float ymf,
                                               float &ax, float &ay, float &az) {
+    // a + (+-d) as fma(d, +-1, a): the product is exact, so the one rounding is the addition's (signed zeros
+    // included), and one sign constant per end replaces an XOR per component
     const uint32_t sj = (uint32_t)(ent & 1) << 31;
-    ax = (float)((double)ax + dxsign(ddiv_fast(q.t0, md, ym), sj));
-    ay = (float)((double)ay + dxsign(ddiv_fast(q.t1, md, ym), sj));
-    az = (float)((double)az + dxsign(ddiv_fast(q.t2, md, ym), sj));
-    const uint32_t sd = sj ^ 0x80000000u;
-    ax = ax + fxsign(fdiv_fast(q.f0, mf, ymf), sd);
-    ay = ay + fxsign(fdiv_fast(q.f1, mf, ymf), sd);
-    az = az + fxsign(fdiv_fast(q.f2, mf, ymf), sd);
+    const double sgn = __hiloint2double((int)(0x3ff00000u | sj), 0);        // +1 at end i, -1 at end j
+    const float sgd = __uint_as_float(0xbf800000u ^ sj);                    // damping: -1 at end i, +1 at end j
+    ax = (float)__builtin_fma(ddiv_fast(q.t0, md, ym), sgn, (double)ax);
+    ay = (float)__builtin_fma(ddiv_fast(q.t1, md, ym), sgn, (double)ay);
+    az = (float)__builtin_fma(ddiv_fast(q.t2, md, ym), sgn, (double)az);
+    ax = __builtin_fmaf(fdiv_fast(q.f0, mf, ymf), sgd, ax);
+    ay = __builtin_fmaf(fdiv_fast(q.f1, mf, ymf), sgd, ay);
+    az = __builtin_fmaf(fdiv_fast(q.f2, mf, ymf), sgd, az);
 }
 
 // Env forces on one mass after its spring terms, each one Point.forced in the reference's order: gravity
@@ -587,12 +590,20 @@ template <int CTRL> __device__ inline float dpp_f(float v) {
 // Sequential float sums ((0 + x_0) + x_1) + ... + x_{M-1} over the walker's M lanes, three at once.
 // Chain: s_q <- s_{q-1} + x_q repeated M-1 times leaves lane base+M-1 holding exactly that left-to-right
 // sum of its own walker (the chain never leaves the walker's lanes); then one broadcast per sum.
+// One chain per loop: three chains in one loop body get SLP-packed into v_pk_add_f32, which cannot take a DPP
+// operand (2 moves + 2 zero fills + 1 packed add for two chains instead of 2 v_add_f32_dpp).
+template <int CTRL>
+__device__ inline float seq_chain(float x, int M) {
+    float a = 0.f + x;
+    for (int t = 1; t < M; t++) a = dpp_f<CTRL>(a) + x;
+    return a;
+}
 __device__ inline void seq_sum3_lanes(float x, float y, float z, int base, int M, float &sx, float &sy, float &sz) {
-    float a = 0.f + x, b = 0.f + y, c = 0.f + z;
+    float a, b, c;
     if (M <= 16) {            // walkers of M | 16 lanes sit inside one 16-lane DPP row
-        for (int t = 1; t < M; t++) { a = dpp_f<0x111>(a) + x; b = dpp_f<0x111>(b) + y; c = dpp_f<0x111>(c) + z; }
+        a = seq_chain<0x111>(x, M); b = seq_chain<0x111>(y, M); c = seq_chain<0x111>(z, M);
     } else {
-        for (int t = 1; t < M; t++) { a = dpp_f<0x138>(a) + x; b = dpp_f<0x138>(b) + y; c = dpp_f<0x138>(c) + z; }
+        a = seq_chain<0x138>(x, M); b = seq_chain<0x138>(y, M); c = seq_chain<0x138>(z, M);
     }
     const int last = base + M - 1;
     sx = lane_get(a, last); sy = lane_get(b, last); sz = lane_get(c, last);
@@ -1142,26 +1153,53 @@ __device__ __forceinline__ float lane_gather(float v, int src_byte) {
 #endif
 // Spring term and damping force of one edge from its endpoints' state (gathered from the mass lanes):
 // spring_edge's arithmetic with the cheaper reciprocal (identical results; cold path unchanged).
+// Cold path: every quantity again with IEEE divisions and numpy's sqrt (exact for every input).
+__device__ __forceinline__ void spring_terms_cold(const EdgeRec &e, float x, float r0, float r1, float r2, double &t0,
+                                               double &t1, double &t2, float &d0, float &d1, float &d2,
+                                               int spring_mode) {
+    const float cur = np_norm3(-r0, -r1, -r2);                      // engine.py:86 (p_i - p_j)
+    const float dx = cur - x;                                       // engine.py:96
+    double dist = (double)cur;                                      // engine.py:73
+    if (CONFIG_R > dist) dist = CONFIG_R;                           // Python max(distance, r), NaN kept
+    const float fsz = (spring_mode == 1 || !(dx < 0.f && edge_string(e.ij))) ? (-dx) * e.k : 0.f;  // :97-100
+    const float nf = -fsz;                                                                           // :75
+    d0 = r0; d1 = r1; d2 = r2;
+    if (cur > 0.f) { d0 = r0 / cur; d1 = r1 / cur; d2 = r2 / cur; }
+    if (spring_mode == 1) {
+        t0 = (double)(fsz * d0); t1 = (double)(fsz * d1); t2 = (double)(fsz * d2);
+    } else {
+        t0 = (double)(nf * r0) / dist; t1 = (double)(nf * r1) / dist; t2 = (double)(nf * r2) / dist;
+    }
+}
+
+// sqrtf of a float s in [2^-96, 2^126): v_sqrt_f32 and the one-ulp correction, the same steps as the compiler's
+// correctly rounded sqrtf minus its small-input rescaling and zero/inf fix-up, which this range never needs
+__device__ __forceinline__ float sqrt_mid(float s) {
+    const float r = __builtin_amdgcn_sqrtf(s);
+    const float rd = __uint_as_float(__float_as_uint(r) - 1u), ru = __uint_as_float(__float_as_uint(r) + 1u);
+    float o = (__builtin_fmaf(-rd, r, s) <= 0.f) ? rd : r;
+    return (__builtin_fmaf(-ru, r, s) > 0.f) ? ru : o;
+}
+
 __device__ __forceinline__ void spring_terms(const EdgeRec &e, float x, float pix, float piy, float piz, float pjx,
                                              float pjy, float pjz, float vix, float viy, float viz, float vjx,
                                              float vjy, float vjz, double &t0, double &t1, double &t2, float &g0,
                                              float &g1, float &g2, int spring_mode) {
-    const float cur = np_norm3(pix - pjx, piy - pjy, piz - pjz);   // engine.py:86
-    const float dx = cur - x;                                       // engine.py:96
     const float r0 = pjx - pix, r1 = pjy - piy, r2 = pjz - piz;     // other.pos - self.pos
+    float d0, d1, d2;
 #if WG_FAST_SPRING
-    // max(distance, r) as v_max_f64: it differs from Python's max only for a NaN distance, which the cold path
-    // below recomputes (the fast path needs cur >= r anyway)
-    double dist = __builtin_fmax((double)cur, CONFIG_R);
-#else
-    double dist = (double)cur;                                      // engine.py:73
-    if (CONFIG_R > dist) dist = CONFIG_R;                           // max(distance, r)
-#endif
+    // np.linalg.norm(p_i - p_j) (engine.py:86): squares summed in float64, rounded, sqrt.  (p_i - p_j)^2 == r^2.
+    const float sq = (float)(((double)(r0 * r0) + (double)(r1 * r1)) + (double)(r2 * r2));
+    const bool mid = sq >= 0x1p-96f && sq < 0x1p126f;                // false for NaN
+    const float cur = sqrt_mid(sq);
+    const float dx = cur - x;                                       // engine.py:96
+    // cur >= 2^-48 > Config.r: max(distance, r) is the distance itself
+    const double dist = (double)cur;
     const double yc = rcp64_nr(dist);
     const float fsz = (spring_mode == 1 || !(dx < 0.f && edge_string(e.ij))) ? (-dx) * e.k : 0.f;  // :97-100
     const float nf = -fsz;                                                                           // :75
     const float ycf = (float)yc;
-    float d0 = fdiv_fast(r0, cur, ycf), d1 = fdiv_fast(r1, cur, ycf), d2 = fdiv_fast(r2, cur, ycf);
+    d0 = fdiv_fast(r0, cur, ycf); d1 = fdiv_fast(r1, cur, ycf); d2 = fdiv_fast(r2, cur, ycf);
     if (spring_mode == 1) {
         t0 = (double)(fsz * d0); t1 = (double)(fsz * d1); t2 = (double)(fsz * d2);
     } else {
@@ -1169,28 +1207,13 @@ __device__ __forceinline__ void spring_terms(const EdgeRec &e, float x, float pi
         t1 = ddiv_fast((double)(nf * r1), dist, yc);
         t2 = ddiv_fast((double)(nf * r2), dist, yc);
     }
-#if WG_FAST_SPRING
-    // the quotients are exact when the distance is unclamped (cur >= r) and every quotient is finite; a non-finite
-    // one (or NaN distance) makes its sum non-finite (|d| <= 1 cannot overflow a sum of three)
-    const bool fast_ok = (double)cur >= CONFIG_R && __builtin_isfinite(d0 + d1 + d2) && __builtin_isfinite(t0 + t1 + t2);
+    // the quotients are exact when every one is finite; a non-finite one makes its sum non-finite (|d| <= 1
+    // cannot overflow a sum of three)
+    const bool fast_ok = mid && __builtin_isfinite(d0 + d1 + d2) && __builtin_isfinite(t0 + t1 + t2);
+    if (__builtin_expect(!fast_ok, 0)) spring_terms_cold(e, x, r0, r1, r2, t0, t1, t2, d0, d1, d2, spring_mode);
 #else
-    const bool fast_ok = cur > 0.f && (double)cur == dist && __builtin_isfinite(d0) && __builtin_isfinite(d1) &&
-                         __builtin_isfinite(d2) && __builtin_isfinite(t0) && __builtin_isfinite(t1) &&
-                         __builtin_isfinite(t2);
+    spring_terms_cold(e, x, r0, r1, r2, t0, t1, t2, d0, d1, d2, spring_mode);
 #endif
-    if (__builtin_expect(!fast_ok, 0)) {
-#if WG_FAST_SPRING
-        dist = (double)cur;
-        if (CONFIG_R > dist) dist = CONFIG_R;                       // Python max(distance, r), NaN kept
-#endif
-        d0 = r0; d1 = r1; d2 = r2;
-        if (cur > 0.f) { d0 = r0 / cur; d1 = r1 / cur; d2 = r2 / cur; }
-        if (spring_mode == 1) {
-            t0 = (double)(fsz * d0); t1 = (double)(fsz * d1); t2 = (double)(fsz * d2);
-        } else {
-            t0 = (double)(nf * r0) / dist; t1 = (double)(nf * r1) / dist; t2 = (double)(nf * r2) / dist;
-        }
-    }
     const float dk = np_dot3(vix - vjx, viy - vjy, viz - vjz, d0, d1, d2);  // optimized_walker.py:102-103
     const float dkc = dk * e.c;                                               // :104
     g0 = dkc * d0; g1 = dkc * d1; g2 = dkc * d2;
@@ -2117,7 +2140,8 @@ int launch_lean(const wg_batch *b, const KParams &kp, bool in3d, const float *a,
                 const wg_outputs &o, const LeanGeo &g, hipStream_t st) {
     const int blocks = lean_blocks(b, g);
     const int ne = (g.wpw * b->K + 63) / 64;
-    const int lds = g.wpb * g.slice;
+    // WG_LDS_PAD (diagnostic): extra LDS bytes per workgroup, to measure the kernel at lower occupancy
+    const int lds = g.wpb * g.slice + std::max(0, env_int("WG_LDS_PAD", 0));
 #define WG_LAUNCH_LEAN(D3, NE_)                                                                                  \
     hipLaunchKernelGGL((walker_step_lean<D3, NE_>), dim3(blocks), dim3(64 * g.wpb), lds, st, *b, kp, a, cols,   \
                        astride, o, g)

@@ -1109,7 +1109,7 @@ struct LeanGeo {
     int wpb;                                  // waves per workgroup
     int lgM;                                  // log2(M)
     int slice;                                // LDS bytes per wave
-    int off_df, off_inc, off_x;               // byte offsets in the slice (spring terms / obs tile at 0)
+    int off_df, off_inc, off_x;               // byte offsets in the slice (spring terms at 0)
     int pl;                                   // entries per spring-term plane (SoA; >= wpw * K, even)
     float invK, invA, invM;                   // invM = 1/M, exact (M | 64 is a power of two)
 };
@@ -1423,6 +1423,7 @@ __device__ __forceinline__ void pair_forces(const wg_batch &b, const KParams &kp
 #ifndef WG_LEAN_SOA
 #define WG_LEAN_SOA 0
 #endif
+
 #if WG_LEAN_SOA
 typedef TermsSoA LeanTerms;
 __device__ __forceinline__ LeanTerms lean_terms(char *sl, const LeanGeo &lg) {
@@ -1442,12 +1443,11 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
                                              const LeanGeo &lg, char *sl, const LeanTile &t, int lane,
                                              const LeanIn<NE> &L) {
     const int M = b.M, K = b.K, A = b.A;
-    const int w0 = t.w0, nw = t.nw, nE = t.nE;
+    const int w0 = t.w0, nE = t.nE;
     const int wl = t.wl, q = t.q, mu_wl = t.mu_wl, mu_ua = t.mu_ua;
     const bool is_mass = t.is_mass, is_mus = t.is_mus, acts = t.acts;
     const uint32_t pl = t.P0 + lane, ul = t.U0 + lane;   // this lane's mass / muscle
-    // slice: spring terms t (f64 x3) | df (f32 x3) | incidence words | muscle x; the obs tile aliases the spring
-    // terms once the masses are done
+    // slice: spring terms t (f64 x3) | df (f32 x3) | incidence words | muscle x
     const LeanTerms ts = lean_terms(sl, lg);
 #ifdef WG_STAMPS
     const int stamp_wave = blockIdx.x * lg.wpb + (threadIdx.x >> 6);
@@ -1599,23 +1599,28 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
     STAMP(5);
     // ================= observation rows: Creature.getstat (gym/optimized_walker.py:129-162) =========
     if (o.obs && !(WG_ABLATE & 16)) {
+        // straight from registers: lane q's 3d values are one contiguous piece of its walker's row, stored as d-float
+        // vectors; the wave's pieces tile the rows, and the L2 merges them into whole lines
         constexpr int d = IN3D ? 3 : 2, per = 3 * d;
         const int stride = o.obs_stride, nmid = kp.conmid ? 3 : 0;
-        float *otile = reinterpret_cast<float *>(sl);
-        wave_sync();                      // every lane is done reading the spring terms
+        typedef float fvd __attribute__((ext_vector_type(d), aligned(4)));
         if (is_mass) {
-            float *row = otile + wl * stride + per * q;
-            const float pm[3] = {px, py, pz}, vm[3] = {vx, vy, vz}, am[3] = {ax, ay, az};
+            float *wrow = o.obs + (uint32_t)(w0 + wl) * (uint32_t)stride;
             // G1 getstat (midform 2, gym/walker.py:88-96) subtracts the SUM of positions
             const float mm[3] = {kp.midform == 2 ? sx : midx, kp.midform == 2 ? sy : midy, kp.midform == 2 ? sz : midz};
+            const float pm[3] = {px, py, pz}, vm[3] = {vx, vy, vz}, am[3] = {ax, ay, az};
+            fvd vp, vv, va;
 #pragma unroll
             for (int c = 0; c < d; c++) {
-                row[c] = kp.midform ? (pm[c] - mm[c]) * kp.pk : pm[c] * kp.pk;
-                row[d + c] = vm[c] * kp.vk;
-                row[2 * d + c] = am[c] * kp.ak;
+                vp[c] = kp.midform ? (pm[c] - mm[c]) * kp.pk : pm[c] * kp.pk;
+                vv[c] = vm[c] * kp.vk;
+                va[c] = am[c] * kp.ak;
             }
+            float *dst = wrow + per * q;   // (a 3-vector's type is 16 B: no array indexing over fvd)
+            *reinterpret_cast<fvd *>(dst) = vp;
+            *reinterpret_cast<fvd *>(dst + d) = vv;
+            *reinterpret_cast<fvd *>(dst + 2 * d) = va;
             if (q == 0) {
-                float *wrow = otile + wl * stride;
                 if (nmid) {
                     wrow[per * M] = kp.midform ? mm[0] : 0.f; wrow[per * M + 1] = kp.midform ? mm[1] : 0.f;
                     wrow[per * M + 2] = kp.midform ? mm[2] : 0.f;
@@ -1623,17 +1628,7 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
                 for (int r = per * M + nmid + A; r < stride; r++) wrow[r] = 0.f;
             }
         }
-        if (is_mus) otile[mu_wl * stride + per * M + nmid + mu_ua] = x * kp.mk;
-        wave_sync();
-        float *ob = o.obs + (uint32_t)w0 * (uint32_t)stride;
-        const int n = nw * stride;
-        if (((((uintptr_t)ob) & 15) == 0) && (n & 3) == 0) {
-            const float4 *s4 = reinterpret_cast<const float4 *>(otile);
-            float4 *d4 = reinterpret_cast<float4 *>(ob);
-            for (int i = lane; i < (n >> 2); i += 64) d4[i] = s4[i];
-        } else {
-            for (int i = lane; i < n; i += 64) ob[i] = otile[i];
-        }
+        if (is_mus) o.obs[(uint32_t)(w0 + mu_wl) * (uint32_t)stride + per * M + nmid + mu_ua] = x * kp.mk;
     }
     STAMP(6);
 #ifdef WG_STAMPS
@@ -2119,9 +2114,8 @@ bool lean_geo(const wg_batch *b, int obs_stride, LeanGeo *out, int spring_mode =
     g.wpb = (wpb == 1 || wpb == 2) ? wpb : 4;
     const int ew = g.wpw * b->K;                          // springs of a full wave tile
     g.pl = (ew + 3) & ~3;                                 // plane length: 16-B aligned f64 and f32 planes
-    const int obs_b = g.wpw * std::max(0, obs_stride) * 4;
-    // t (f64 x3) | df (f32 x3) | incidence words | x; the obs tile aliases t
-    g.off_df = align16(std::max(g.pl * 24, obs_b));
+    // t (f64 x3) | df (f32 x3) | incidence words | x (observation rows go from registers to HBM, no LDS tile)
+    g.off_df = align16(g.pl * 24);
     g.off_inc = g.off_df + align16(g.pl * 12);
     g.off_x = g.off_inc + align16(ew * 4);
     g.slice = g.off_x + align16(std::max(1, g.wpw * b->A) * 4);
@@ -2389,7 +2383,7 @@ int wg_launch_geometry(const wg_batch *b, wg_launch_info *info) {
     if (rc) return rc;
     if (!info) return fail(WG_EINVAL, "null info");
     LeanGeo lg{};
-    if (lean_geo(b, 0, &lg)) {   // the step kernel of uniform M | 64 batches (the obs tile may widen the slice)
+    if (lean_geo(b, 0, &lg)) {   // the step kernel of uniform M | 64 batches
         info->threads = 64 * lg.wpb;
         info->walkers_per_block = lg.wpb * lg.wpw;
         info->blocks = lean_blocks(b, lg);

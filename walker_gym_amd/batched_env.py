@@ -281,11 +281,14 @@ class BatchedPhysicsEnv:
         """Walker ranges run() steps on separate streams (ragged batches: ranges of plan blocks).  Default 2 for
         batches of >= 2^19 masses: measured on the canonical 65,536-walker bench (2^20 masses), 36.5 us/step
         with 2 ranges against 42.9 with 1 and 49.0 with 4; on 65,536 Balance-v0 walkers (2^18 masses, a 13 us
-        launch) 2 ranges lose slightly, 13.7 against 13.3 (scripts/lanes_ab.py; bit-identical results).
-        WG_LANES overrides."""
+        launch) 2 ranges lose slightly, 13.7 against 13.3 (scripts/lanes_ab.py; bit-identical results).  Pair
+        forces (O(M^2) per walker) make launches long at fewer masses: 4,096 chain walkers of 100 masses (2^18.6),
+        175 us/step with 2 ranges against 210 with 1 (profiles/r02_ab_pair_markstein_chain.json), so those
+        batches take 2 ranges from 2^17 masses.  WG_LANES overrides."""
         if lanes is None:
             env = os.environ.get("WG_LANES")
-            lanes = int(env) if env else (2 if self.batch.P >= (1 << 19) else 1)
+            heavy = int(self.params.pair_mode) != 0
+            lanes = int(env) if env else (2 if self.batch.P >= (1 << (17 if heavy else 19)) else 1)
         if lanes < 1:
             raise ValueError("lanes must be >= 1")
         if self.batch.ragged:

@@ -247,6 +247,16 @@ __device__ inline double ddiv_exact(double a, double b, double y) {
     if (!__builtin_isfinite(q) || y == 0.0) return q;
     return __builtin_fma(__builtin_fma(-q, b, a), y, q);
 }
+// a / b for a float64 a and a b whose value is a float32 (y = RN64(1/b)): Markstein's quotient when it lands in
+// [2^-800, 2^800] (scripts/check_division.c case 2; with |b| in float32 range, a and every intermediate are then
+// normal doubles), a zero numerator as a * y (the IEEE sign), anything else by IEEE division.
+__device__ inline double ddiv_f32d(double a, double b, double y) {
+    const double q = a * y;
+    const double m = __builtin_fma(__builtin_fma(-q, b, a), y, q);
+    const double am = __builtin_fabs(m);
+    if (__builtin_expect(am >= 0x1p-800 && am <= 0x1p800, 1)) return m;
+    return a == 0.0 ? q : a / b;
+}
 
 // Global -> LDS copy of n 4-byte words (16-B vector loads when both ends allow it).
 template <typename T4, typename T1>
@@ -373,19 +383,31 @@ template <class TS>
 __device__ __forceinline__ IncTerm inc_term(const TS &ts, int lb, int ent) { return ts.get(lb + (ent >> 1)); }
 // a = f32(f64(a) + t/m) (Point.forced with a float64 force, engine.py:67,75), then the damping pair
 // p1.forced(-df), p2.forced(df) (optimized_walker.py:105-106); end j sees the opposite signs.
+template <bool FMA_SIGN>
 __device__ __forceinline__ void acc_f64_entry(const IncTerm &q, int ent, double md, double ym, float mf, float ymf,
                                               float &ax, float &ay, float &az) {
-    // a + (+-d) as fma(d, +-1, a): the product is exact, so the one rounding is the addition's (signed zeros
-    // included), and one sign constant per end replaces an XOR per component
     const uint32_t sj = (uint32_t)(ent & 1) << 31;
-    const double sgn = __hiloint2double((int)(0x3ff00000u | sj), 0);        // +1 at end i, -1 at end j
-    const float sgd = __uint_as_float(0xbf800000u ^ sj);                    // damping: -1 at end i, +1 at end j
-    ax = (float)__builtin_fma(ddiv_fast(q.t0, md, ym), sgn, (double)ax);
-    ay = (float)__builtin_fma(ddiv_fast(q.t1, md, ym), sgn, (double)ay);
-    az = (float)__builtin_fma(ddiv_fast(q.t2, md, ym), sgn, (double)az);
-    ax = __builtin_fmaf(fdiv_fast(q.f0, mf, ymf), sgd, ax);
-    ay = __builtin_fmaf(fdiv_fast(q.f1, mf, ymf), sgd, ay);
-    az = __builtin_fmaf(fdiv_fast(q.f2, mf, ymf), sgd, az);
+    if (FMA_SIGN) {
+        // a + (+-d) as fma(d, +-1, a): the product is exact, so the one rounding is the addition's (signed zeros
+        // included), and one sign constant per end replaces an XOR per component (5 fewer VALU per entry, 5 more
+        // registers: the register-tight wave kernels keep the XOR form)
+        const double sgn = __hiloint2double((int)(0x3ff00000u | sj), 0);        // +1 at end i, -1 at end j
+        const float sgd = __uint_as_float(0xbf800000u ^ sj);                    // damping: -1 at end i, +1 at end j
+        ax = (float)__builtin_fma(ddiv_fast(q.t0, md, ym), sgn, (double)ax);
+        ay = (float)__builtin_fma(ddiv_fast(q.t1, md, ym), sgn, (double)ay);
+        az = (float)__builtin_fma(ddiv_fast(q.t2, md, ym), sgn, (double)az);
+        ax = __builtin_fmaf(fdiv_fast(q.f0, mf, ymf), sgd, ax);
+        ay = __builtin_fmaf(fdiv_fast(q.f1, mf, ymf), sgd, ay);
+        az = __builtin_fmaf(fdiv_fast(q.f2, mf, ymf), sgd, az);
+    } else {
+        ax = (float)((double)ax + dxsign(ddiv_fast(q.t0, md, ym), sj));
+        ay = (float)((double)ay + dxsign(ddiv_fast(q.t1, md, ym), sj));
+        az = (float)((double)az + dxsign(ddiv_fast(q.t2, md, ym), sj));
+        const uint32_t sd = sj ^ 0x80000000u;
+        ax = ax + fxsign(fdiv_fast(q.f0, mf, ymf), sd);
+        ay = ay + fxsign(fdiv_fast(q.f1, mf, ymf), sd);
+        az = az + fxsign(fdiv_fast(q.f2, mf, ymf), sd);
+    }
 }
 
 // Env forces on one mass after its spring terms, each one Point.forced in the reference's order: gravity
@@ -455,7 +477,7 @@ __device__ __forceinline__ void mass_tail(const KParams &kp, float mf, float ymf
 // per edge — gym/optimized_walker.py:124-127 with gym/engine.py:65-76, 101-102), then gravity, linear
 // damping and the ground penalty (gym/env.py:31-41 / gym/optimized_env.py:146-172, each one
 // Point.forced), then Point.run1 (gym/engine.py:174-178).  Returns the new state and old_a.
-template <class TS>
+template <class TS, bool FMA_SIGN = true>
 __device__ __forceinline__ void mass_accumulate(const TS &ts, const uint16_t *inc, int lb, int s0, int s1, float mf,
                                                 float &ax, float &ay, float &az, int spring_mode) {
     const double md = (double)mf;
@@ -495,12 +517,12 @@ __device__ __forceinline__ void mass_accumulate(const TS &ts, const uint16_t *in
                 B = inc_term(ts, lb, eb);
                 const int ea2 = inc[min(r + 2, rl)];
                 __builtin_amdgcn_sched_barrier(0);   // keep the reads above the arithmetic
-                acc_f64_entry(A, ea, md, ym, mf, ymf, ax, ay, az);
+                acc_f64_entry<FMA_SIGN>(A, ea, md, ym, mf, ymf, ax, ay, az);
                 if (r + 1 >= s1) break;
                 A = inc_term(ts, lb, ea2);
                 const int eb2 = inc[min(r + 3, rl)];
                 __builtin_amdgcn_sched_barrier(0);
-                acc_f64_entry(B, eb, md, ym, mf, ymf, ax, ay, az);
+                acc_f64_entry<FMA_SIGN>(B, eb, md, ym, mf, ymf, ax, ay, az);
                 ea = ea2; eb = eb2;
                 // opaque hand-over: stops the phi-of-loads fold that would sink A's reads to its use
                 asm volatile("" : "+v"(A.t0), "+v"(A.t1), "+v"(A.t2), "+v"(A.f0), "+v"(A.f1), "+v"(A.f2), "+v"(ea), "+v"(eb));
@@ -634,6 +656,45 @@ __device__ inline float pw_sum_lanes(float x, int base, int M, int lane) {
     return r;
 }
 
+// ------------------------------------------------------------------ pair terms
+// One gravity / coulomb partner (gym/engine.py:128-147 -> anti_forced :69-76 -> forced :65-67), all float64:
+// r = max(norm(d) as float64, Config.r); f = -c*s_lo*s_hi / r**2; a = f32(f64(a) + ((-f)*d / r) / m).  The
+// divisions by r (when unclamped: a float32 value) and by m go through ddiv_f32d with one IEEE reciprocal each.
+__device__ __forceinline__ void pair_central_term(double coef, double slo, double shi, float d0, float d1, float d2,
+                                                  double md, double ym, float &ax, float &ay, float &az) {
+    const double cur = (double)np_norm3(d0, d1, d2);   // == norm(p_i - p_j): the squares do not see the sign
+    const double r = CONFIG_R > cur ? CONFIG_R : cur;
+    const double f = ((-coef) * slo) * shi / (r * r);
+    const double nf = -f;
+    double t0 = nf * (double)d0, t1 = nf * (double)d1, t2 = nf * (double)d2;
+    if (__builtin_expect(r == cur, 1)) {
+        const double yr = 1.0 / r;
+        t0 = ddiv_f32d(t0, r, yr); t1 = ddiv_f32d(t1, r, yr); t2 = ddiv_f32d(t2, r, yr);
+    } else {                                           // clamped (or NaN) distance: IEEE
+        t0 = t0 / r; t1 = t1 / r; t2 = t2 / r;
+    }
+    ax = (float)((double)ax + ddiv_f32d(t0, md, ym));
+    ay = (float)((double)ay + ddiv_f32d(t1, md, ym));
+    az = (float)((double)az + ddiv_f32d(t2, md, ym));
+}
+// One colliding bounce partner: resilience(i, r_s + r_i, k/2) seen from this end (gym/engine.py:78-102), the
+// float64 force path with the float32 numerator nf * d.
+__device__ __forceinline__ void bounce_term(float cur, float nf, float d0, float d1, float d2, double md, double ym,
+                                            float &ax, float &ay, float &az) {
+    const double dc = (double)cur;
+    const double dist = CONFIG_R > dc ? CONFIG_R : dc;
+    double t0 = (double)(nf * d0), t1 = (double)(nf * d1), t2 = (double)(nf * d2);
+    if (__builtin_expect(dist == dc, 1)) {
+        const double yd = 1.0 / dist;
+        t0 = ddiv_f32d(t0, dist, yd); t1 = ddiv_f32d(t1, dist, yd); t2 = ddiv_f32d(t2, dist, yd);
+    } else {
+        t0 = t0 / dist; t1 = t1 / dist; t2 = t2 / dist;
+    }
+    ax = (float)((double)ax + ddiv_f32d(t0, md, ym));
+    ay = (float)((double)ay + ddiv_f32d(t1, md, ym));
+    az = (float)((double)az + ddiv_f32d(t2, md, ym));
+}
+
 // ------------------------------------------------------------------ pair passes from LDS (workgroup kernel)
 // SURVEY §8(f) 3 for walkers the lean kernel does not take (M not dividing 64, M > 64, ragged batches): the
 // arithmetic of pair_central / pair_bounce (lean kernel, below) with the partners' positions read from the tile's
@@ -643,6 +704,7 @@ __device__ void pair_forces_lds(const wg_batch &b, const KParams &kp, const floa
                                 int M, int q, size_t g0, float mf, float &ax, float &ay, float &az) {
     const float *p3 = spos + 3 * (lm + q);
     const double md = (double)mf;
+    const double ym = 1.0 / md;                  // every "/ m" below: ddiv_f32d (m is a float32 value)
     for (int pass = 0; pass < 2; pass++) {   // gym/engine.py:128-137 (Config.g, m) and :139-147 (Config.k, e)
         if (!(kp.pair_mode & (1 << pass))) continue;
         const double coef = pass == 0 ? kp.pair_g : kp.pair_k;
@@ -652,13 +714,7 @@ __device__ void pair_forces_lds(const wg_batch &b, const KParams &kp, const floa
             const float *o3 = spos + 3 * (lm + pj);
             const double os = pass == 0 ? (double)sm[lm + pj] : (b.charge ? b.charge[g0 + pj] : kp.pair_e);
             const float d0 = o3[0] - p3[0], d1 = o3[1] - p3[1], d2 = o3[2] - p3[2];   // partner - self
-            double r = (double)np_norm3(d0, d1, d2);
-            if (CONFIG_R > r) r = CONFIG_R;
-            const double slo = pj < q ? os : sq, shi = pj < q ? sq : os;
-            const double f = ((-coef) * slo) * shi / (r * r);
-            ax = (float)((double)ax + ((-f) * (double)d0 / r) / md);
-            ay = (float)((double)ay + ((-f) * (double)d1 / r) / md);
-            az = (float)((double)az + ((-f) * (double)d2 / r) / md);
+            pair_central_term(coef, pj < q ? os : sq, pj < q ? sq : os, d0, d1, d2, md, ym, ax, ay, az);
         }
     }
     if (kp.pair_mode & 4) {                  // gym/engine.py:114-125, partners j < q, then j != q, then j > q
@@ -674,11 +730,7 @@ __device__ void pair_forces_lds(const wg_batch &b, const KParams &kp, const floa
                 if (!((double)cur <= x)) continue;
                 const float dx = cur - (float)x;                                  // engine.py:96
                 const float nf = -((-dx) * kp.bounce_kh);                         // -f_size, :75,100
-                double dist = (double)cur;
-                if (CONFIG_R > dist) dist = CONFIG_R;
-                ax = (float)((double)ax + (double)(nf * d0) / dist / md);
-                ay = (float)((double)ay + (double)(nf * d1) / dist / md);
-                az = (float)((double)az + (double)(nf * d2) / dist / md);
+                bounce_term(cur, nf, d0, d1, d2, md, ym, ax, ay, az);
             }
         }
     }
@@ -1350,20 +1402,14 @@ __device__ __forceinline__ double lane_gather_d(double v, int src_byte) {
 __device__ __forceinline__ void pair_central(double coef, double sq, const float *p3, float mf, int lane, int M,
                                              bool is_mass, float &ax, float &ay, float &az) {
     const int gb = lane & ~(M - 1), q = lane & (M - 1);
-    const double md = (double)mf;
+    const double md = (double)mf, ym = 1.0 / md;
     for (int pj = 0; pj < M; pj++) {
         const int src = (gb + pj) << 2;
         const float ox = lane_gather(p3[0], src), oy = lane_gather(p3[1], src), oz = lane_gather(p3[2], src);
         const double os = lane_gather_d(sq, src);
         if (!is_mass || pj == q) continue;
         const float d0 = ox - p3[0], d1 = oy - p3[1], d2 = oz - p3[2];   // partner - self
-        double r = (double)np_norm3(d0, d1, d2);      // == norm(p_i - p_j): the squares do not see the sign
-        if (CONFIG_R > r) r = CONFIG_R;
-        const double slo = pj < q ? os : sq, shi = pj < q ? sq : os;
-        const double f = ((-coef) * slo) * shi / (r * r);
-        ax = (float)((double)ax + ((-f) * (double)d0 / r) / md);
-        ay = (float)((double)ay + ((-f) * (double)d1 / r) / md);
-        az = (float)((double)az + ((-f) * (double)d2 / r) / md);
+        pair_central_term(coef, pj < q ? os : sq, pj < q ? sq : os, d0, d1, d2, md, ym, ax, ay, az);
     }
 }
 
@@ -1377,7 +1423,7 @@ __device__ __forceinline__ void pair_central(double coef, double sq, const float
 __device__ __forceinline__ void pair_bounce(float kh, double rs, const float *p3, float mf, int lane, int M,
                                             bool is_mass, float &ax, float &ay, float &az) {
     const int gb = lane & ~(M - 1), q = lane & (M - 1);
-    const double md = (double)mf;
+    const double md = (double)mf, ym = 1.0 / md;
     for (int ph = 0; ph < 3; ph++) {
         for (int pj = 0; pj < M; pj++) {
             const int src = (gb + pj) << 2;
@@ -1391,11 +1437,7 @@ __device__ __forceinline__ void pair_bounce(float kh, double rs, const float *p3
             if (!((double)cur <= x)) continue;
             const float dx = cur - (float)x;                                  // engine.py:96
             const float nf = -((-dx) * kh);                                   // -f_size, :75,100
-            double dist = (double)cur;
-            if (CONFIG_R > dist) dist = CONFIG_R;
-            ax = (float)((double)ax + (double)(nf * d0) / dist / md);
-            ay = (float)((double)ay + (double)(nf * d1) / dist / md);
-            az = (float)((double)az + (double)(nf * d2) / dist / md);
+            bounce_term(cur, nf, d0, d1, d2, md, ym, ax, ay, az);
         }
     }
 }
@@ -1816,7 +1858,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
     float px = 0.f, py = 0.f, pz = 0.f, vx = 0.f, vy = 0.f, vz = 0.f, ax = 0.f, ay = 0.f, az = 0.f;
     bool hit = false;
     if (is_mass) {
-        mass_accumulate(ts, reinterpret_cast<const uint16_t *>(s_inc) + 2 * mlb, mlb, io0, io1, mf, ax, ay, az, 0);
+        mass_accumulate<TermsAoS, (NE > 1)>(ts, reinterpret_cast<const uint16_t *>(s_inc) + 2 * mlb, mlb, io0, io1, mf, ax,
+                                            ay, az, 0);
         mass_tail(kp, mf, (float)ym, p3, v3, px, py, pz, vx, vy, vz, ax, ay, az, hit, pin != 0);
         const uint32_t pl = (uint32_t)(P0 + lane);
         float *gpo = b.pos + 3 * (size_t)pl, *gvo = b.vel + 3 * (size_t)pl, *gao = b.acc + 3 * (size_t)pl;

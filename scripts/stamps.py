@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Phase timeline of the lean kernel from a -DWG_STAMPS build (profiling aid, not product).
+"""Phase timeline of the lean kernel (or, WG_WORKLOAD=ragged, the ragged wave kernel) from a -DWG_STAMPS build
+(profiling aid, not product).
 
     python scripts/variant_ab.py build stamps=-DWG_STAMPS     # here
     python scripts/stamps.py [build_ab/lib_stamps.so]         # GPU box: one full-batch canonical launch
@@ -24,13 +25,14 @@ from walker_gym_amd import _lib  # noqa: E402
 from walker_gym_amd.batched_env import BatchedPhysicsEnv  # noqa: E402
 
 N = int(os.environ.get("WG_N", "65536"))
-spec, params = make_spec("canonical", N, seed=1000)
+WORKLOAD = os.environ.get("WG_WORKLOAD", "canonical")     # canonical (lean kernel) or ragged (wave kernel)
+spec, params = make_spec(WORKLOAD, N, seed=1000)
 env = BatchedPhysicsEnv(spec, device="cuda:0", **params)
-acts = (torch.rand((60, N, 8), device="cuda:0") * 2 - 1).contiguous()
+acts = (torch.rand((60, N, max(1, env.batch.A)), device="cuda:0") * 2 - 1).contiguous()
 env.run(acts[:50].contiguous(), 50, lanes=1)          # past the free fall, as in the bench's timed region
 env.run(acts[50:51].contiguous(), 1, lanes=1)
 torch.cuda.synchronize()
-W = N // 4
+W = env.batch.plan_blocks if env.batch.ragged else N * env.batch.M // 64   # waves (one tile each)
 st = np.zeros((W, 8), np.uint64)
 print("WG_LEAN_WAVES", os.environ.get("WG_LEAN_WAVES", "4"))
 L = _lib.load()

@@ -1750,6 +1750,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int tile = blockIdx.x * rg.wpb + wv;
     if (tile >= ntiles) return;
+#ifdef WG_STAMPS
+    const int stamp_wave = tile;
+#endif
+    STAMP(0);
     char *sl = smem + wv * rg.slice;
     const TermsAoS ts{reinterpret_cast<double *>(sl), reinterpret_cast<float *>(sl + rg.off_df)};
     uint32_t *s_inc = reinterpret_cast<uint32_t *>(sl + rg.off_inc);
@@ -1817,6 +1821,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
     float act = 0.f;
     if (acts) act = action[(size_t)s_row[uw] * action_stride + ua];
     if (kp.prio) __builtin_amdgcn_s_setprio(0);
+    STAMP(1);
 
     // ================= incidence lists into LDS; act (gym/optimized_walker.py:27-43,164-172)
 #pragma unroll
@@ -1832,6 +1837,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
     if (is_mus) s_x[lane] = x;
     const double ym = 1.0 / (double)mf;
     wave_sync();
+    STAMP(2);
 
     // ================= springs: gym/engine.py:78-102 + gym/optimized_walker.py:92-106 =================
 #pragma unroll
@@ -1853,12 +1859,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
             spring_edge_regs(e, le, xr, pix, piy, piz, pjx, pjy, pjz, vix, viy, viz, vjx, vjy, vjz, ts, 0);
     }
     wave_sync();
+    STAMP(3);
 
     // ================= masses: ordered accumulation, env forces, Point.run1 =================
     float px = 0.f, py = 0.f, pz = 0.f, vx = 0.f, vy = 0.f, vz = 0.f, ax = 0.f, ay = 0.f, az = 0.f;
     bool hit = false;
     if (is_mass) {
-        mass_accumulate<TermsAoS, (NE > 1)>(ts, reinterpret_cast<const uint16_t *>(s_inc) + 2 * mlb, mlb, io0, io1, mf, ax,
+        mass_accumulate<TermsAoS, false>(ts, reinterpret_cast<const uint16_t *>(s_inc) + 2 * mlb, mlb, io0, io1, mf, ax,
                                             ay, az, 0);
         mass_tail(kp, mf, (float)ym, p3, v3, px, py, pz, vx, vy, vz, ax, ay, az, hit, pin != 0);
         const uint32_t pl = (uint32_t)(P0 + lane);
@@ -1869,6 +1876,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
         if (b.contact) b.contact[pl] = (uint8_t)hit;
         if (b.radius) b.radius[pl] = hit ? 3.0 : 1.0;   // gym/optimized_env.py:156,175
     }
+    STAMP(4);
     wave_sync();                       // every lane is done reading the spring terms: their region takes the
     if (is_mass) {                     // per-mass reduction terms, the damping region the walker partials
         const float nv = np_norm3(vx, vy, vz);
@@ -1924,54 +1932,58 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
         }
         if (o.energy) o.energy[wrow] = 0.5f * rd[5] + rd[6];
     }
+    STAMP(5);
 
     // ================= observation rows: Creature.getstat (gym/optimized_walker.py:129-162) =========
-    // Walker w's row is per*M_w values, the 3 conmid values, A_w muscle lengths, then zeros to the stride; its
-    // first per*M_w + nmid + A_w values are staged at per*mo_w + nmid*w + uo_w in LDS (the spring-term region).
+    // Walker w's row (the caller's row s_row[w]) is per*M_w values, the 3 conmid values, A_w muscle lengths, then
+    // zeros to the stride.  Each mass lane stores its 3d values straight from registers as d-float pieces, each
+    // muscle lane its length; the padding is written only when the caller's buffer is not known to be clean.
     if (o.obs) {
         constexpr int d = IN3D ? 3 : 2, per = 3 * d;
         const int stride = o.obs_stride, nmid = kp.conmid ? 3 : 0;
-        float *stg = reinterpret_cast<float *>(sl);
+        typedef float fvd __attribute__((ext_vector_type(d), aligned(4)));
         if (is_mass) {
             const float *rd = s_red + 8 * mw;
             const float fM = (float)mM;
-            float *row = stg + per * mlm + nmid * mw + s_uo[mw] + per * (lane - mlm);
+            float *dst = o.obs + (size_t)s_row[mw] * stride + per * (lane - mlm);
             const float pm[3] = {px, py, pz}, vm[3] = {vx, vy, vz}, am[3] = {ax, ay, az};
+            fvd vp, vv, va;
 #pragma unroll
             for (int c = 0; c < d; c++) {
                 const float mid = kp.midform == 2 ? rd[c] : rd[c] / fM;   // G1 getstat: the SUM
-                row[c] = kp.midform ? (pm[c] - mid) * kp.pk : pm[c] * kp.pk;
-                row[d + c] = vm[c] * kp.vk;
-                row[2 * d + c] = am[c] * kp.ak;
+                vp[c] = kp.midform ? (pm[c] - mid) * kp.pk : pm[c] * kp.pk;
+                vv[c] = vm[c] * kp.vk;
+                va[c] = am[c] * kp.ak;
             }
+            *reinterpret_cast<fvd *>(dst) = vp;        // (a 3-vector's type is 16 B: no array indexing over fvd)
+            *reinterpret_cast<fvd *>(dst + d) = vv;
+            *reinterpret_cast<fvd *>(dst + 2 * d) = va;
         }
         if (lane < nw && nmid) {
             const int M = s_mo[lane + 1] - s_mo[lane];
-            float *row = stg + per * s_mo[lane + 1] + nmid * lane + s_uo[lane];
+            float *row = o.obs + (size_t)wrow * stride + per * M;
             const float *rd = s_red + 8 * lane;
             for (int c = 0; c < 3; c++) row[c] = kp.midform == 2 ? rd[c] : kp.midform ? rd[c] / (float)M : 0.f;
         }
-        if (is_mus) stg[per * s_mo[uw + 1] + nmid * (uw + 1) + s_uo[uw] + ua] = x * kp.mk;
-        wave_sync();
-        if (o.obs_pad_clean) {
-            // the rows' padding is already zero: each walker's own values only, one row after the other
-            for (int w = 0; w < nw; w++) {
-                const int base = per * s_mo[w] + nmid * w + s_uo[w];
-                const int len = per * (s_mo[w + 1] - s_mo[w]) + nmid + (s_uo[w + 1] - s_uo[w]);
-                float *dst = o.obs + (size_t)s_row[w] * stride;
-                for (int c = lane; c < len; c += 64) dst[c] = stg[base + c];
-            }
-        } else {
-            // nw whole rows of `stride` floats (zero padded) to the caller's rows; row w = i / stride
+        if (is_mus) o.obs[(size_t)s_row[uw] * stride + per * (s_mo[uw + 1] - s_mo[uw]) + nmid + ua] = x * kp.mk;
+        if (!o.obs_pad_clean) {
+            // zeros from each row's own length to the stride; row w = i / stride
             const float inv = 1.f / (float)stride;
             for (int i = lane; i < nw * stride; i += 64) {
                 const int w = fdiv(i, stride, inv), c = i - w * stride;
-                const int base = per * s_mo[w] + nmid * w + s_uo[w];
                 const int len = per * (s_mo[w + 1] - s_mo[w]) + nmid + (s_uo[w + 1] - s_uo[w]);
-                o.obs[(size_t)s_row[w] * stride + c] = c < len ? stg[base + c] : 0.f;
+                if (c >= len) o.obs[(size_t)s_row[w] * stride + c] = 0.f;
             }
         }
     }
+    STAMP(6);
+#ifdef WG_STAMPS
+    if (lane == 0 && stamp_wave < (1 << 16)) {   // slot 7: HW_ID (gfx9 hwreg 4) | XCC_ID (gfx940+ hwreg 20) << 32
+        const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+        const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+        g_stamps[stamp_wave * 8 + 7] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
+    }
+#endif
 }
 
 // reset: v += noise, steps = 0 (PhysicsEnv.reset, gym/optimized_env.py:53-68).  zmode 0: x, y (2D);

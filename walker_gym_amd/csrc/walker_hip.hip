@@ -1466,6 +1466,7 @@ __device__ __forceinline__ void pair_forces(const wg_batch &b, const KParams &kp
 #define WG_LEAN_SOA 0
 #endif
 
+
 #if WG_LEAN_SOA
 typedef TermsSoA LeanTerms;
 __device__ __forceinline__ LeanTerms lean_terms(char *sl, const LeanGeo &lg) {
@@ -1877,9 +1878,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
         if (b.radius) b.radius[pl] = hit ? 3.0 : 1.0;   // gym/optimized_env.py:156,175
     }
     STAMP(4);
+    // contacts after run1 and the all-stopped test, one bit per mass lane (walker w: lanes [s_mo[w], s_mo[w + 1]))
+    const float nvm = is_mass ? np_norm3(vx, vy, vz) : 0.f;
+    const unsigned long long hb = __ballot(is_mass && (py - kp.ground < 0.f));
+    const unsigned long long sb = __ballot(is_mass && nvm < 0.1f);
     wave_sync();                       // every lane is done reading the spring terms: their region takes the
     if (is_mass) {                     // per-mass reduction terms, the damping region the walker partials
-        const float nv = np_norm3(vx, vy, vz);
+        const float nv = nvm;
         s_tp[3 * lane] = px; s_tp[3 * lane + 1] = py; s_tp[3 * lane + 2] = pz;
         s_tn[lane] = nv;
         s_tk[lane] = mf * (nv * nv);   // numpy's float32 ** 2 is libm powf: may differ by 1 ulp
@@ -1889,18 +1894,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
 
     // ================= per-walker reductions, 8 lanes per walker (numpy's summation orders) ==========
     // r 0-2: sequential sums of pos[:, r] (getstat mid / info centroid); r 3: pairwise y (np.mean);
-    // r 4-6: pairwise |v|, m|v|^2, m*g*(y - ground); r 7: contact count << 1 | all-stopped
+    // r 4-6: pairwise |v|, m|v|^2, m*g*(y - ground); r 7: contact count << 1 | all-stopped, from the ballots
     for (int idx = lane; idx < nw * 8; idx += 64) {
         const int w = idx >> 3, r = idx & 7;
         const int lm = s_mo[w], M = s_mo[w + 1] - lm;
         float v;
         if (r == 7) {
-            int hits = 0, all = 1;
-            for (int q = 0; q < M; q++) {
-                hits += (s_tp[3 * (lm + q) + 1] - kp.ground < 0.f);
-                all &= (s_tn[lm + q] < 0.1f);
-            }
-            v = __int_as_float((hits << 1) | all);
+            const unsigned long long wm = (M == 64) ? ~0ull : (((1ull << M) - 1ull) << lm);
+            v = __int_as_float((__popcll(hb & wm) << 1) | ((sb & wm) == wm ? 1 : 0));
         } else if (r < 3) {
             v = 0.f;
             for (int q = 0; q < M; q++) v += s_tp[3 * (lm + q) + r];

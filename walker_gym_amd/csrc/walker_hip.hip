@@ -2163,6 +2163,12 @@ bool lean_geo(const wg_batch *b, int obs_stride, LeanGeo *out, int spring_mode =
         return false;
     LeanGeo g{};
     g.wpw = 64 / M;
+    // small batches: fewer walkers per wave until there are 512 wave tiles (two per CU), so a latency-bound step
+    // spreads over more waves (4,096 Balance-v0 walkers: 16 -> 8 walkers per wave, 6.40 -> 5.97 us per step,
+    // profiles/r02_ab_balance4096_wpw.json); WG_LEAN_WPW (experiment) caps the count
+    while (g.wpw > 1 && (b->N + g.wpw - 1) / g.wpw < 512) g.wpw >>= 1;
+    const int wcap = env_int("WG_LEAN_WPW", 0);
+    if (wcap > 0 && wcap < g.wpw) g.wpw = wcap;
     g.lgM = 0;
     while ((1 << g.lgM) < M) g.lgM++;
     if ((g.wpw * b->K + 63) / 64 > 8 || g.wpw * b->A > 64) return false;

@@ -1197,12 +1197,6 @@ __device__ __forceinline__ float lane_gather(float v, int src_byte) {
 #ifndef WG_FAST_SPRING
 #define WG_FAST_SPRING 1
 #endif
-#ifndef WG_SPRING_PIPE
-#define WG_SPRING_PIPE 0
-#endif
-#ifndef WG_LEAN_WAVES
-#define WG_LEAN_WAVES 6   // waves per SIMD the lean kernel's register budget targets (NE < 8)
-#endif
 // Spring term and damping force of one edge from its endpoints' state (gathered from the mass lanes):
 // spring_edge's arithmetic with the cheaper reciprocal (identical results; cold path unchanged).
 // Cold path: every quantity again with IEEE divisions and numpy's sqrt (exact for every input).
@@ -1521,8 +1515,8 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
 
     // ================= springs: gym/engine.py:78-102 + gym/optimized_walker.py:92-106 =================
     // endpoint state from the mass lanes by ds_bpermute: every lane takes part (inactive sources read as 0).
-    // WG_SPRING_PIPE: the gathers of pass it + 1 are issued before the arithmetic of pass it, so their LDS
-    // latency overlaps it (12 more registers).
+    // (Issuing pass it + 1's gathers before pass it's arithmetic needs 90 VGPRs, 5 waves per SIMD: 48.5 against
+    // 47.8 us per launch, profiles/r02_ab_spring_pipe.json.)
     struct Gath { float v[12]; };
     auto gather = [&](int it, Gath &g) {
         const int le = lane + 64 * it;
@@ -1554,27 +1548,15 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
             }
         }
     };
-#if WG_SPRING_PIPE
-    Gath g[2];                                             // double buffer: pass it reads g[it & 1]
-    gather(0, g[0]);
 #pragma unroll
     for (int it = 0; it < NE; it++) {
         // no early loop exit: it keeps er[] in registers (a reference under a `break` made hipcc park the rest
         // lengths in scratch right after their loads, serialising them)
         if (64 * it >= nE) continue;                       // wave-uniform
-        if (it + 1 < NE && 64 * (it + 1) < nE) gather(it + 1, g[(it + 1) & 1]);
-        __builtin_amdgcn_sched_barrier(0);                 // the next pass's gathers stay above this arithmetic
-        spring(it, g[it & 1]);
-    }
-#else
-#pragma unroll
-    for (int it = 0; it < NE; it++) {
-        if (64 * it >= nE) continue;                       // wave-uniform
         Gath g;
         gather(it, g);
         spring(it, g);
     }
-#endif
     if (WG_LOAD_ORDER) {
 #pragma unroll
         for (int it = 0; it < NE; it++)
@@ -1685,7 +1667,7 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
 
 // NE spring passes per wave need up to 8 x 16-B records in registers: 6 waves per SIMD hold up to NE 4 without
 // spills, NE 8 (up to 512 springs per 64 lanes) gets the 4-wave register budget.
-constexpr int lean_waves(int NE) { return NE >= 8 ? 4 : WG_LEAN_WAVES; }
+constexpr int lean_waves(int NE) { return NE >= 8 ? 4 : 6; }
 
 // One tile (64 / M walkers) per wave; waves never wait for one another.
 template <bool IN3D, int NE>

@@ -2217,11 +2217,10 @@ bool rag_geo(const wg_batch *b, int obs_stride, RagGeo *out) {
     const int wpb = env_int("WG_LEAN_WAVES", 4);
     g.wpb = (wpb == 1 || wpb == 2) ? wpb : 4;
     const int ec = 64 * ne;                                      // spring slots of a tile
-    const int stage = 4 * (9 * 64 + 3 * RW_MAXW + 64);           // obs staging (aliases the spring terms)
-    (void)obs_stride;
-    // spring terms t (f64 x3), later the per-mass reduction terms, then the obs staging | damping forces df,
-    // later the walker partials | incidence words | muscle x | walker offsets and rows
-    g.off_df = align16(std::max(std::max(ec * 24, stage), 4 * 64 * 6));
+    (void)obs_stride;                                            // observation rows go from registers to HBM
+    // spring terms t (f64 x3), later the per-mass reduction terms | damping forces df, later the walker partials |
+    // incidence words | muscle x | walker offsets and rows
+    g.off_df = align16(std::max(ec * 24, 4 * 64 * 6));
     g.off_inc = g.off_df + align16(std::max(ec * 12, 4 * RW_MAXW * 8));
     g.off_x = g.off_inc + align16(ec * 4);
     g.off_wo = g.off_x + align16(64 * 4);

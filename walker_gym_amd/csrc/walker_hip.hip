@@ -1703,8 +1703,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lean_waves(
 // muscles, RW_MAXW walkers and 64 * NE springs in all.  One wave per tile and no workgroup barrier, with the lean
 // kernel's arithmetic: one mass per lane (the tile's walkers side by side), the springs in NE passes of 64 lanes
 // with the endpoints' state gathered by ds_bpermute, each mass lane walking its incidence list in reference
-// order.  What differs from the uniform lean kernel is bookkeeping: a lane finds its walker by a binary search
-// over the tile's walker offsets in LDS; per-walker reductions run 8 lanes per walker over an LDS copy of the
+// order.  What differs from the uniform lean kernel is bookkeeping: a lane finds its walker by counting the walker
+// starts at or below it (v_readlane of the walker lanes' offsets); per-walker reductions run 8 lanes per walker over an LDS copy of the
 // per-mass terms in numpy's orders (as walker_step_kernel); observation rows are assembled in LDS and streamed to
 // the caller's rows (wg_batch.row), zero padded to the stride.
 constexpr int RW_MAXW = 32;   // walkers per wave tile (planner cap)
@@ -1715,14 +1715,6 @@ struct RagGeo {
     int off_df, off_inc, off_x, off_wo;   // byte offsets in the slice (spring terms at 0)
 };
 
-__device__ __forceinline__ int wave_locate(const int *off, int n, int x) {   // largest w < n with off[w] <= x
-    int lo = 0, hi = n - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (off[mid] <= x) lo = mid; else hi = mid - 1;
-    }
-    return lo;
-}
 
 template <bool IN3D, int NE>
 // LDS: ~5.8 KB per wave at NE 2 (27 waves per CU); NE 4 / 8 tiles need more LDS and registers
@@ -1790,16 +1782,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
     // lane -> walker maps (tile-local offsets in LDS)
     if (lane <= nw) { s_mo[lane] = wmo; s_eo[lane] = weo; s_uo[lane] = wuo; }
     if (lane < nw) s_row[lane] = wrow;
+    // lane -> walker maps by counting the walker starts at or below the lane: the starts are in the walker lanes'
+    // registers (v_readlane, no LDS round trips; a tile has few walkers); NE spring passes map their edge slots too
+    int mw = 0, uw = 0, eww[NE];
+#pragma unroll
+    for (int it = 0; it < NE; it++) eww[it] = 0;
+    for (int w = 1; w < nw; w++) {
+        const int so = __builtin_amdgcn_readlane(wmo, w), se = __builtin_amdgcn_readlane(weo, w);
+        const int su = __builtin_amdgcn_readlane(wuo, w);
+        mw += lane >= so;
+        uw += lane >= su;
+#pragma unroll
+        for (int it = 0; it < NE; it++) eww[it] += lane + 64 * it >= se;
+    }
+    if (!is_mass) mw = 0;
+    if (!is_mus) uw = 0;
     wave_sync();
-    const int mw = is_mass ? wave_locate(s_mo, nw, lane) : 0;            // this lane's mass: walker
     const int mlm = s_mo[mw], mM = s_mo[mw + 1] - mlm, mlb = s_eo[mw];
     int io0 = 0, io1 = 0;
     if (is_mass) {
         const uint32_t io = (uint32_t)(P0 + lane) + (uint32_t)(w0 + mw);   // inc_off: M_w + 1 per walker
         io0 = b.inc_off[io]; io1 = b.inc_off[io + 1];
     }
-    const int uw = is_mus ? wave_locate(s_uo, nw, lane) : 0;             // this lane's muscle: walker
-    const int ua = lane - s_uo[uw];
+    const int ua = lane - s_uo[uw];                                      // this lane's muscle in walker uw
     const bool acts = action != nullptr && is_mus && ua < action_cols;
     float act = 0.f;
     if (acts) act = action[(size_t)s_row[uw] * action_stride + ua];
@@ -1828,7 +1833,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
         if (64 * it >= nE) continue;                       // wave-uniform
         const int le = lane + 64 * it;
         const EdgeRec e = er[it];
-        const int ew_w = wave_locate(s_eo, nw, min(le, max(nE - 1, 0)));
+        const int ew_w = le < nE ? eww[it] : 0;
         const int elm = s_mo[ew_w], ew = le - s_eo[ew_w], eA = s_uo[ew_w + 1] - s_uo[ew_w];
         const int bi = (elm + edge_i(e.ij)) << 2, bj = (elm + edge_j(e.ij)) << 2;
         const float pix = lane_gather(p3[0], bi), piy = lane_gather(p3[1], bi), piz = lane_gather(p3[2], bi);

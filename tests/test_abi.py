@@ -135,3 +135,50 @@ def test_launch_geometry_canonical(lib):
     assert lib.wg_launch_geometry(C.byref(b), C.byref(info)) == 0
     assert info.threads == 256 and info.walkers_per_block == 16 and info.blocks == 4096
     assert info.lds_bytes <= 32768   # five workgroups per CU (160 KiB LDS)
+
+
+def test_wave_edge_passes(lib):
+    """Spring passes of a wave tile (walker_hip.hip wave_passes): enough for the longest walker and for 64 masses of
+    the densest one, rounded to an instantiated count; 0 = the batch cannot use the wave kernel."""
+    for (M, K), ne in {(32, 64): 2, (16, 40): 3, (4, 5): 2, (8, 4): 1, (64, 300): 8, (64, 512): 8,
+                       (65, 10): 0, (4, 600): 0, (2, 20): 0}.items():
+        assert lib.wg_wave_edge_passes(M, K) == ne, (M, K)
+
+
+def test_plan_waves_host(lib):
+    rng = np.random.default_rng(1)
+    N = 3000
+    Ms = rng.integers(1, 33, N); Ks = np.minimum(rng.integers(0, 2 * Ms + 1), 64); As = Ks // 5
+    mo = np.concatenate([[0], np.cumsum(Ms)]).astype(np.int32)
+    eo = np.concatenate([[0], np.cumsum(Ks)]).astype(np.int32)
+    uo = np.concatenate([[0], np.cumsum(As)]).astype(np.int32)
+    ne = lib.wg_wave_edge_passes(int(Ms.max()), int(Ks.max()))
+    assert ne > 0
+    plan = np.zeros(N + 1, np.int32)
+    args = (mo.ctypes.data_as(C.c_void_p), eo.ctypes.data_as(C.c_void_p), uo.ctypes.data_as(C.c_void_p), N)
+    nt = lib.wg_plan_waves(*args, plan.ctypes.data_as(C.c_void_p), N + 1)
+    assert nt > 0 and plan[0] == 0 and plan[nt] == N
+    a, b = plan[:nt], plan[1:nt + 1]
+    assert np.all(b > a) and np.all(b - a <= 32)                       # RW_MAXW walkers per tile
+    assert np.all(mo[b] - mo[a] <= 64) and np.all(uo[b] - uo[a] <= 64) and np.all(eo[b] - eo[a] <= 64 * ne)
+    # greedy and maximal: the next walker would not have fitted any tile but the last
+    nxt = b[:-1]
+    full = ((mo[nxt + 1] - mo[a[:-1]] > 64) | (eo[nxt + 1] - eo[a[:-1]] > 64 * ne) | (uo[nxt + 1] - uo[a[:-1]] > 64)
+            | (nxt + 1 - a[:-1] > 32))
+    assert np.all(full)
+    small = np.zeros(2, np.int32)
+    assert lib.wg_plan_waves(*args, small.ctypes.data_as(C.c_void_p), 1) == _lib.WG_ERANGE
+    big = np.array([0, 65], np.int32)
+    assert lib.wg_plan_waves(big.ctypes.data_as(C.c_void_p), np.array([0, 4], np.int32).ctypes.data_as(C.c_void_p),
+                             np.array([0, 0], np.int32).ctypes.data_as(C.c_void_p), 1,
+                             small.ctypes.data_as(C.c_void_p), 1) == _lib.WG_EINVAL
+
+
+def test_launch_geometry_small_batch_halves_tiles(lib):
+    """A uniform batch with fewer than 512 full wave tiles gets fewer walkers per wave (two tiles per CU)."""
+    b = _lib.WgBatch(N=4096, M=4, K=5, A=2, ragged=0)
+    for f in ("pos", "vel", "acc", "mass", "edges", "inc", "inc_off", "muscle_x", "steps"):
+        setattr(b, f, 16)
+    info = _lib.WgLaunchInfo()
+    assert lib.wg_launch_geometry(C.byref(b), C.byref(info)) == 0
+    assert info.walkers_per_block == 4 * 8 and info.blocks == 128        # 8 Balance walkers per wave, 512 tiles

@@ -179,7 +179,8 @@ def load_traffic(workload: str, walkers: int):
     """HBM bytes per full-batch launch from a committed rocprofv3 PMC run (profiles/*pmc*.json), if present."""
     import glob
     best = None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), key=os.path.getmtime):   # newest last
+    # newest round last: the round tags (r01_, r02a_, r02c_, ...) sort by name (mtimes do not survive every copy)
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
         try:
             d = json.load(open(f))
         except Exception:

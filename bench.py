@@ -47,6 +47,8 @@ def parse(argv=None):
     ap.add_argument("--workload", default="canonical", choices=["canonical", "balance", "ragged", "chain"])
     ap.add_argument("--chain-points", type=int, default=100, help="masses per chain walker (--workload chain)")
     ap.add_argument("--lanes", type=int, default=None, help="walker ranges on separate streams (default: auto)")
+    ap.add_argument("--resident", action="store_true", help="also time the K steps as ONE wg_rollout launch (state in "
+                    "registers across steps; open-loop actions) and report it beside the line (not the headline)")
     ap.add_argument("--graph", action="store_true", help="time a HIP-graph replay of the K steps (and the direct "
                                                          "calls beside it)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -280,6 +282,15 @@ def main():
             env.run(acts[:n1], n1, lanes=1)
             single_ms = timed(env, acts[:n1], n1, 1, stream)
         direct_ms = timed(env, acts, args.steps, lanes, stream) if graph is not None else None
+        resident_ms = None
+        if args.resident:
+            env.run(acts[:n1], n1, lanes=lanes, resident=True)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            env.run(acts, args.steps, lanes=lanes, resident=True)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            resident_ms = e0.elapsed_time(e1) / args.steps
         D = env.obs_dim
         B = bytes_per_walker_step(env.batch.host, bool(params.get("in3d")))
         M, K = env.batch.M, env.batch.K
@@ -331,6 +342,13 @@ def main():
         if graph is not None:
             line["graph"] = {"replay_ms_per_step": round(step_ms, 5), "direct_ms_per_step": round(direct_ms, 5),
                              "launch_overhead_share": round(max(0.0, 1 - step_ms / direct_ms), 4)}
+        if resident_ms is not None:
+            line["resident_rollout"] = {
+                "ms_per_step": round(resident_ms, 5), "env_steps_per_s": round(N * 1e3 / resident_ms, 1),
+                "lanes": lanes,
+                "note": "the same K steps as ONE wg_rollout launch per walker range: state in registers across steps, "
+                        "per-step obs/reward/done/info written every step (open-loop actions known up front); not the "
+                        "headline, which is one launch per env step (SURVEY 8(d))"}
         if tr:
             line["roofline"]["traffic_source"] = tr.get("source")
         if args.workload == "chain":

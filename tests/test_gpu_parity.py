@@ -391,6 +391,45 @@ def test_rollout_equals_stepwise():
         assert np.array_equal(rw.cpu().numpy(), r[t].cpu().numpy())
 
 
+@pytest.mark.parametrize("case", ["canonical", "balance2d_discrete", "run2_pinned", "canonical_long_lanes2"])
+def test_resident_rollout_bit_identical(case):
+    """wg_rollout (one launch, state in registers across steps) == wg_step per step: every step's obs / reward /
+    done and the final state (pos, vel, acc, muscle x, steps, contact), bit for bit."""
+    import torch
+    from walker_gym_amd.batched_env import BatchedPhysicsEnv
+    from walker_gym_amd.synthetic import canonical_walkers
+    from walker_gym_amd.walker import create_balance_creature, creatures_to_spec, replicate_spec
+    T, lanes, params = 25, 1, dict(in3d=1)
+    if case.startswith("canonical"):
+        N = 3000 if case == "canonical" else 20000
+        spec = canonical_walkers(N, seed=11)
+        if case == "canonical_long_lanes2":
+            T, lanes = 130, 2          # past steps > 100: the all-stopped done branch is live
+    elif case == "balance2d_discrete":
+        N = 5000
+        spec = replicate_spec(creatures_to_spec([create_balance_creature()]), N)
+        params = dict(in3d=0, action_mode=1)
+    else:
+        N = 4096
+        spec = canonical_walkers(N, seed=12)
+        spec["pinned"] = (np.random.default_rng(12).random(len(spec["m"])) < 0.05).astype(np.uint8)
+        params = dict(in3d=1, integrator=2)
+    A = int(spec["n_muscles"].max())
+    acts = np.random.default_rng(13).uniform(-1, 1, (T, N, A)).astype(np.float32)
+    if params.get("action_mode") == 1:
+        acts = np.where(acts > 0, 1.0, 0.0).astype(np.float32)
+    got = []
+    for resident in (False, True):
+        env = BatchedPhysicsEnv(spec, **params)
+        o, r, d = env.rollout(acts, lanes=lanes, resident=resident)
+        torch.cuda.synchronize()
+        st = env.batch.state_dict()
+        got.append([o.cpu(), r.cpu(), d.cpu()] + [t.cpu() for t in st.values()])
+    assert len(got[0]) == len(got[1])
+    for k, (a, b) in enumerate(zip(*got)):   # NaN == NaN: a walker that blows up does so on both paths
+        assert np.array_equal(a.numpy(), b.numpy(), equal_nan=a.dtype.is_floating_point), (case, k)
+
+
 def test_run_lanes_bit_identical():
     """run() with the walkers split over 2 / 3 streams (lanes) gives the same bits as one stream."""
     import torch

@@ -223,8 +223,11 @@ class BatchedPhysicsEnv:
                              self.batch.plan_blocks, self._stream()), "wg_step")
         return self.obs, self.reward, self.done.bool(), self.info()
 
-    def rollout(self, actions, obs_out=None, reward_out=None, done_out=None, lanes: Optional[int] = None):
-        """T steps in one C call (T back-to-back launches, no host sync); outputs for every step."""
+    def rollout(self, actions, obs_out=None, reward_out=None, done_out=None, lanes: Optional[int] = None,
+                resident: bool = True):
+        """T steps in one C call, no host sync; outputs for every step.  resident (default): wg_rollout, one launch
+        for all T steps where the batch allows it (uniform M | 64, no pair forces), each walker's state kept in
+        registers between steps; False: wg_step, one launch per step.  Bit-identical either way."""
         if not isinstance(actions, torch.Tensor):
             actions = torch.as_tensor(np.asarray(actions, dtype=np.float32))
         actions = actions.to(self.device, torch.float32).contiguous()
@@ -241,23 +244,25 @@ class BatchedPhysicsEnv:
         require_tensor(reward_out, "reward_out", dv, torch.float32, (T, self.N))
         require_tensor(done_out, "done_out", dv, torch.uint8, (T, self.N))
         lanes = self._lanes(lanes) if T > 0 else 1
+        entry = "wg_rollout" if resident else "wg_step"
         if lanes > 1:
             self._run_lanes(actions, T, lambda w0, w1: self._outputs(
                 obs_out[0, w0:w1], reward_out[0, w0:w1], done_out[0, w0:w1], None, None,
-                obs_step=self.N * self.obs_dim, out_step=self.N, pad_clean=clean), lanes)
+                obs_step=self.N * self.obs_dim, out_step=self.N, pad_clean=clean), lanes, entry=entry)
             return obs_out, reward_out, done_out
         o = self._outputs(obs_out, reward_out, done_out, None, None, obs_step=self.N * self.obs_dim,
                           out_step=self.N, pad_clean=clean)
-        _lib.check(_lib.load().wg_step(
+        _lib.check(getattr(_lib.load(), entry)(
             C.byref(self.batch.struct), C.byref(self._pstruct), C.c_void_p(actions.data_ptr()), cols, cols,
             self.N * cols, C.byref(o), T,
             None if self.batch.plan is None else C.c_void_p(self.batch.plan.data_ptr()),
-            self.batch.plan_blocks, self._stream()), "wg_step")
+            self.batch.plan_blocks, self._stream()), entry)
         return obs_out, reward_out, done_out
 
-    def run(self, actions, n_steps: int, info: bool = True, lanes: Optional[int] = None):
+    def run(self, actions, n_steps: int, info: bool = True, lanes: Optional[int] = None, resident: bool = False):
         """Throughput path: n_steps env steps in one C call; step s acts with actions[s % T]
-        ([T, N, A] device tensor; T == n_steps or 1) and overwrites obs/reward/done(/info) each step."""
+        ([T, N, A] device tensor; T == n_steps or 1) and overwrites obs/reward/done(/info) each step.  resident:
+        wg_rollout (one launch for all steps where the batch allows it) instead of one launch per step."""
         require_tensor(actions, "actions", self.device, torch.float32)
         if actions.dim() != 3:
             raise ValueError("actions must be a contiguous [n_steps or 1, N, A] device tensor")
@@ -265,17 +270,18 @@ class BatchedPhysicsEnv:
         if n != self.N or T not in (1, n_steps):
             raise ValueError("actions must be a contiguous [n_steps or 1, N, A] device tensor")
         lanes = self._lanes(lanes)
+        entry = "wg_rollout" if resident else "wg_step"
         if lanes > 1:
             return self._run_lanes(actions, int(n_steps), lambda w0, w1: self._outputs(
                 self.obs[w0:w1], self.reward[w0:w1], self.done[w0:w1], self.centroid[w0:w1] if info else None,
-                self.energy[w0:w1] if info else None, pad_clean=True), lanes)
+                self.energy[w0:w1] if info else None, pad_clean=True), lanes, entry=entry)
         o = self._outputs(self.obs, self.reward, self.done, self.centroid if info else None,
                           self.energy if info else None, pad_clean=True)
-        _lib.check(_lib.load().wg_step(
+        _lib.check(getattr(_lib.load(), entry)(
             C.byref(self.batch.struct), C.byref(self._pstruct), C.c_void_p(actions.data_ptr()), cols, cols,
             0 if T == 1 else self.N * cols, C.byref(o), int(n_steps),
             None if self.batch.plan is None else C.c_void_p(self.batch.plan.data_ptr()),
-            self.batch.plan_blocks, self._stream()), "wg_step")
+            self.batch.plan_blocks, self._stream()), entry)
 
     def _lanes(self, lanes: Optional[int]) -> int:
         """Walker ranges run() steps on separate streams (ragged batches: ranges of plan blocks).  Default 2 for
@@ -295,7 +301,7 @@ class BatchedPhysicsEnv:
             return max(1, min(lanes, self.batch.plan_blocks // 64))
         return 1 if self.N < 64 * lanes else lanes
 
-    def _run_lanes(self, actions, n_steps: int, outputs, lanes: int):
+    def _run_lanes(self, actions, n_steps: int, outputs, lanes: int, entry: str = "wg_step"):
         """n_steps with the walkers split into `lanes` contiguous ranges, each stepped by its own stream: the
         ranges are independent, so one range's step t + 1 fills the GPU while another's step t drains (the
         launch tail).  Every walker still takes every step, one launch per step per range; the calling
@@ -326,9 +332,9 @@ class BatchedPhysicsEnv:
             else:
                 sub, o = self.batch.sub_struct(w0, w1), outputs(w0, w1)
                 act, plan, nblk = C.c_void_p(actions.data_ptr() + 4 * w0 * cols), None, 0
-            _lib.check(L.wg_step(C.byref(sub), C.byref(self._pstruct), act, cols, cols,
-                                 0 if T == 1 else self.N * cols, C.byref(o), n_steps, plan, nblk,
-                                 C.c_void_p(st.cuda_stream)), "wg_step")
+            _lib.check(getattr(L, entry)(C.byref(sub), C.byref(self._pstruct), act, cols, cols,
+                                         0 if T == 1 else self.N * cols, C.byref(o), n_steps, plan, nblk,
+                                         C.c_void_p(st.cuda_stream)), entry)
             if i:
                 if not torch.cuda.is_current_stream_capturing():
                     actions.record_stream(st)   # the allocator must not recycle it before the side stream is done

@@ -1475,10 +1475,12 @@ __device__ __forceinline__ LeanTerms lean_terms(char *sl, const LeanGeo &lg) {
 
 // One wave's tile after its loads: the edge lanes leave the spring term t and the damping force df of every
 // edge in LDS, then each mass lane walks its incidence list, dividing by m as the reference does (mass_step).
-template <bool IN3D, int NE>
+// RES (walker_rollout_lean): the tile's state stays in L across steps; it is written to HBM only when `last`.
+template <bool IN3D, int NE, bool RES = false>
 __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &kp, const wg_outputs &o,
                                              const LeanGeo &lg, char *sl, const LeanTile &t, int lane,
-                                             const LeanIn<NE> &L) {
+                                             LeanIn<NE> &L, bool last = true) {
+    const bool store = !RES || last;
     const int M = b.M, K = b.K, A = b.A;
     const int w0 = t.w0, nE = t.nE;
     const int wl = t.wl, q = t.q, mu_wl = t.mu_wl, mu_ua = t.mu_ua;
@@ -1496,7 +1498,7 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
 
     // ================= act (gym/optimized_walker.py:27-43,164-172); the incidence lists go to LDS after the
     // springs (WG_LOAD_ORDER 1: their loads are still in flight while the springs run)
-    if (!WG_LOAD_ORDER) {
+    if (!WG_LOAD_ORDER && !RES) {   // (the resident kernel writes them once, before its first step)
 #pragma unroll
         for (int it = 0; it < NE; it++)
             if (lane + 64 * it < nE) s_inc[lane + 64 * it] = L.gi[it];
@@ -1506,7 +1508,7 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
         x = (kp.action_mode == 1) ? ((L.a != 0.f) ? x + L.stp : x - L.stp) : x + L.a;
         if (L.lo > x) x = L.lo;     // Python max(x, originx*minl)
         if (L.hi < x) x = L.hi;     // Python min(x, originx*maxl)
-        b.muscle_x[ul] = x;
+        if (store) b.muscle_x[ul] = x;
     }
     if (is_mus) s_x[lane] = x;
     const double ym = 1.0 / (double)mf;   // IEEE 1/m of this lane's mass: every /m below is exact from it
@@ -1572,12 +1574,14 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
     if (is_mass) {
         const int r1 = (WG_ABLATE & 2) ? min(L.io1, L.io0 + 1) : L.io1;
         const int lb = wl * K;
-        mass_accumulate(ts, reinterpret_cast<const uint16_t *>(s_inc) + 2 * lb, lb, L.io0, r1, mf, ax, ay, az, 0);
+        // (the resident kernel keeps the XOR sign form: 5 fewer registers where its carried state is live)
+        mass_accumulate<LeanTerms, !RES>(ts, reinterpret_cast<const uint16_t *>(s_inc) + 2 * lb, lb, L.io0, r1, mf, ax,
+                                         ay, az, 0);
     }
     if (kp.pair_mode) pair_forces(b, kp, L.p3, mf, pl, lane, M, is_mass, ax, ay, az);   // every lane (gathers)
     if (is_mass) {
         mass_tail(kp, mf, (float)ym, L.p3, L.v3, px, py, pz, vx, vy, vz, ax, ay, az, hit, pin);
-        if (b.radius) b.radius[pl] = hit ? 3.0 : 1.0;   // p.r = 3 / p.r = 1 (gym/optimized_env.py:156,175)
+        if (b.radius && store) b.radius[pl] = hit ? 3.0 : 1.0;   // p.r = 3 / p.r = 1 (gym/optimized_env.py:156,175)
         nv = np_norm3(vx, vy, vz);
         ke = mf * (nv * nv);   // numpy's float32 ** 2 is libm powf: may differ by 1 ulp
         pe = (float)((double)mf * kp.g) * (py - kp.ground);
@@ -1596,15 +1600,18 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
     // M | 64 is a power of two: x / M == x * (1/M) exactly (the same real number, rounded once)
     const float midx = sx * lg.invM, midy = sy * lg.invM, midz = sz * lg.invM;
     if (is_mass) {
-        float *gpo = b.pos + 3 * (size_t)pl, *gvo = b.vel + 3 * (size_t)pl, *gao = b.acc + 3 * (size_t)pl;
-        gpo[0] = px; gpo[1] = py; gpo[2] = pz;
-        gvo[0] = vx; gvo[1] = vy; gvo[2] = vz;
-        gao[0] = ax; gao[1] = ay; gao[2] = az;
-        if (b.contact) b.contact[pl] = (uint8_t)hit;
+        if (store) {
+            float *gpo = b.pos + 3 * (size_t)pl, *gvo = b.vel + 3 * (size_t)pl, *gao = b.acc + 3 * (size_t)pl;
+            gpo[0] = px; gpo[1] = py; gpo[2] = pz;
+            gvo[0] = vx; gvo[1] = vy; gvo[2] = vz;
+            gao[0] = ax; gao[1] = ay; gao[2] = az;
+            if (b.contact) b.contact[pl] = (uint8_t)hit;
+        }
         if (q == 0) {
             const uint32_t wg = (uint32_t)(w0 + wl);
             const int steps = L.wsteps + 1;
-            b.steps[wg] = steps;
+            if (store) b.steps[wg] = steps;
+            if (RES) L.wsteps = steps;
             const float cy = ysum * lg.invM;
             if (o.reward) {
                 const float vpen = (-(vsum * lg.invM)) * 0.1f;
@@ -1655,6 +1662,11 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
         }
         if (is_mus) o.obs[(uint32_t)(w0 + mu_wl) * (uint32_t)stride + per * M + nmid + mu_ua] = x * kp.mk;
     }
+    if (RES) {   // the next step starts from this one's state (Point.pos/v, Muscle.x), in registers
+        L.p3[0] = px; L.p3[1] = py; L.p3[2] = pz;
+        L.v3[0] = vx; L.v3[1] = vy; L.v3[2] = vz;
+        L.x = x;
+    }
     STAMP(6);
 #ifdef WG_STAMPS
     if (lane == 0 && stamp_wave < (1 << 16)) {   // slot 7: HW_ID (gfx9 hwreg 4) | XCC_ID (gfx940+ hwreg 20) << 32
@@ -1695,6 +1707,61 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lean_waves(
     if (kp.prio) __builtin_amdgcn_s_setprio(0);
     STAMP(1);
     lean_compute<IN3D, NE>(b, kp, o, lg, smem + wv * lg.slice, t, lane, L);
+}
+
+// n_steps env steps in one launch (wg_rollout): the tile's static inputs (spring records, incidence lists, masses,
+// muscle bounds) are loaded once and its state (pos, vel, muscle x, step counter) stays in registers from step to
+// step; each step reads its actions (the next step's are in flight while this one computes) and writes its
+// outputs; pos / vel / acc / contact / muscle x / steps go to HBM after the last step.  Same arithmetic as
+// walker_step_lean, step for step (bit-identical to n_steps single-step launches).
+template <bool IN3D, int NE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4 : 5))) void walker_rollout_lean(
+    wg_batch b, KParams kp, const float *__restrict__ action, int action_cols, int action_stride, int64_t action_step,
+    wg_outputs o, int n_steps, LeanGeo lg) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int tile = blockIdx.x * lg.wpb + wv;
+    if (tile * lg.wpw >= b.N) return;
+#ifdef WG_STAMPS
+    const int stamp_wave = tile;
+#endif
+    const LeanTile t = lean_tile_of(b, action, action_cols, lg, tile, lane);
+    LeanIn<NE> L;
+    if (kp.prio) __builtin_amdgcn_s_setprio(2);
+    lean_load<NE>(b, kp, action, action_stride, t, lane, L);
+    if (kp.prio) __builtin_amdgcn_s_setprio(0);
+    {   // the incidence lists are static: into LDS once
+        uint32_t *s_inc = reinterpret_cast<uint32_t *>(smem + wv * lg.slice + lg.off_inc);
+#pragma unroll
+        for (int it = 0; it < NE; it++)
+            if (lane + 64 * it < t.nE) s_inc[lane + 64 * it] = L.gi[it];
+    }
+#pragma clang loop unroll(disable)
+    for (int s = 0; s < n_steps; s++) {
+        // the lane index made opaque each step: its derived addresses and masks are recomputed in the step (a few
+        // VALU) instead of being hoisted out of the loop and held in registers (spilled) across all of it
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const LeanTile ts = lean_tile_of(b, action, action_cols, lg, tile, ln);
+        float a_next = 0.f;                        // the next step's action, in flight while this step computes
+        if (ts.acts && s + 1 < n_steps)
+            a_next = action[(size_t)(s + 1) * (size_t)action_step +
+                            (size_t)(uint32_t)(ts.w0 + ts.mu_wl) * (uint32_t)action_stride + (uint32_t)ts.mu_ua];
+        wg_outputs os = o;
+        if (os.obs) os.obs += (size_t)s * os.obs_step;
+        if (os.reward) os.reward += (size_t)s * os.out_step;
+        if (os.done) os.done += (size_t)s * os.out_step;
+        if (os.energy) os.energy += (size_t)s * os.out_step;
+        if (os.centroid) os.centroid += 3 * (size_t)s * os.out_step;
+        // the same for the static inputs (the mass's 1/m, the springs' endpoint indices are re-derived per step)
+        asm volatile("" : "+v"(L.mf), "+v"(L.io0), "+v"(L.io1), "+v"(L.lo), "+v"(L.hi), "+v"(L.stp));
+#pragma unroll
+        for (int it = 0; it < NE; it++) asm volatile("" : "+v"(L.er[it].ij), "+v"(L.er[it].rest), "+v"(L.er[it].k),
+                                                     "+v"(L.er[it].c));
+        lean_compute<IN3D, NE, true>(b, kp, os, lg, smem + wv * lg.slice, ts, ln, L, s == n_steps - 1);
+        L.a = a_next;
+        wave_sync();   // this step's LDS reads stay ahead of the next step's writes
+    }
 }
 
 // ------------------------------------------------------------------ ragged wave kernel
@@ -2204,6 +2271,30 @@ int launch_lean(const wg_batch *b, const KParams &kp, bool in3d, const float *a,
     return 0;
 }
 
+int launch_lean_rollout(const wg_batch *b, const KParams &kp, bool in3d, const float *a, int cols, int astride,
+                        int64_t astep, const wg_outputs &o, int n_steps, const LeanGeo &g, hipStream_t st) {
+    const int blocks = lean_blocks(b, g);
+    const int ne = (g.wpw * b->K + 63) / 64;
+    const int lds = g.wpb * g.slice;
+#define WG_LAUNCH_RO(D3, NE_)                                                                                    \
+    hipLaunchKernelGGL((walker_rollout_lean<D3, NE_>), dim3(blocks), dim3(64 * g.wpb), lds, st, *b, kp, a, cols, \
+                       astride, astep, o, n_steps, g)
+#define WG_RO_NE(D3)                                                                                             \
+    do {                                                                                                         \
+        if (ne <= 1) WG_LAUNCH_RO(D3, 1);                                                                        \
+        else if (ne == 2) WG_LAUNCH_RO(D3, 2);                                                                   \
+        else if (ne == 3) WG_LAUNCH_RO(D3, 3);                                                                   \
+        else if (ne == 4) WG_LAUNCH_RO(D3, 4);                                                                   \
+        else WG_LAUNCH_RO(D3, 8);                                                                                \
+    } while (0)
+    if (in3d) WG_RO_NE(true); else WG_RO_NE(false);
+#undef WG_RO_NE
+#undef WG_LAUNCH_RO
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(WG_EHIP, "launch failed: %s", hipGetErrorString(e));
+    return 0;
+}
+
 // ---- ragged wave kernel (wg_batch.ragged = 2): spring passes, planner, geometry, launch
 // Spring passes of a wave tile from the batch maxima: enough for the longest walker, and for 64 masses of the
 // densest one (K / M springs per mass), rounded up to an instantiated NE (1, 2, 3, 4, 8); 0 = not eligible.
@@ -2279,7 +2370,7 @@ int dispatch(const wg_batch *b, const KParams &kp, bool in3d, const float *a, in
 
 int run(const wg_batch *b, const wg_params *p, const float *action, int32_t cols, int32_t astride,
         int64_t astep, const wg_outputs *o, int32_t n_steps, const int32_t *plan, int32_t plan_blocks,
-        hipStream_t stream, bool step) {
+        hipStream_t stream, bool step, bool resident = false) {
     int rc = validate(b);
     if (rc) return rc;
     if (!p) return fail(WG_EINVAL, "null params");
@@ -2308,6 +2399,9 @@ int run(const wg_batch *b, const wg_params *p, const float *action, int32_t cols
         return fail(WG_EINVAL, "pair_mode %d needs spring_mode 0", p->pair_mode);
     if (step && (p->pair_mode & 4) && !b->radius)
         return fail(WG_EINVAL, "pair_mode 4 (bounce) needs the radius array");
+    if (resident && use_lean && p->pair_mode == 0)   // one launch for every step, state in registers throughout
+        return launch_lean_rollout(b, kp, p->in3d != 0, action, cols, astride, action ? astep : 0, out, n_steps, lg,
+                                   stream);
     for (int s = 0; s < n_steps; s++) {
         wg_outputs os = out;
         if (os.obs) os.obs += s * os.obs_step;
@@ -2344,6 +2438,13 @@ int wg_step(const wg_batch *b, const wg_params *p, const float *action, int32_t 
             int32_t action_stride, int64_t action_step, const wg_outputs *o, int32_t n_steps,
             const int32_t *plan, int32_t plan_blocks, hipStream_t stream) {
     return run(b, p, action, action_cols, action_stride, action_step, o, n_steps, plan, plan_blocks, stream, true);
+}
+
+int wg_rollout(const wg_batch *b, const wg_params *p, const float *action, int32_t action_cols,
+               int32_t action_stride, int64_t action_step, const wg_outputs *o, int32_t n_steps,
+               const int32_t *plan, int32_t plan_blocks, hipStream_t stream) {
+    return run(b, p, action, action_cols, action_stride, action_step, o, n_steps, plan, plan_blocks, stream, true,
+               true);
 }
 
 int wg_observe(const wg_batch *b, const wg_params *p, const wg_outputs *o, const int32_t *plan,

@@ -46,12 +46,13 @@ def time_one(lib, workload, steps=200, warm=20):
     env = BatchedPhysicsEnv(spec, device="cuda:0", **params)
     acts = (torch.rand((steps, n, env.batch.A), device="cuda:0") * 2 - 1).contiguous()
     res = {}
+    resident = os.environ.get("WG_AB_RESIDENT", "0") == "1"   # time run(resident=True): one launch for all steps
     for lanes in (1, 2):
-        env.run(acts[:warm].contiguous(), warm, lanes=lanes)
+        env.run(acts[:warm].contiguous(), warm, lanes=lanes, resident=resident)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        env.run(acts, steps, lanes=lanes)
+        env.run(acts, steps, lanes=lanes, resident=resident)
         e1.record()
         torch.cuda.synchronize()
         res[f"lanes{lanes}"] = e0.elapsed_time(e1) / steps * 1e3

@@ -1715,7 +1715,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lean_waves(
 // outputs; pos / vel / acc / contact / muscle x / steps go to HBM after the last step.  Same arithmetic as
 // walker_step_lean, step for step (bit-identical to n_steps single-step launches).
 template <bool IN3D, int NE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4 : 5))) void walker_rollout_lean(
+#ifndef WG_RES_WAVES
+#define WG_RES_WAVES 5   // waves per SIMD the resident kernel's register budget targets (its state stays live)
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4 : WG_RES_WAVES))) void walker_rollout_lean(
     wg_batch b, KParams kp, const float *__restrict__ action, int action_cols, int action_stride, int64_t action_step,
     wg_outputs o, int n_steps, LeanGeo lg) {
     extern __shared__ __attribute__((aligned(16))) char smem[];

@@ -284,10 +284,10 @@ def main():
         direct_ms = timed(env, acts, args.steps, lanes, stream) if graph is not None else None
         resident_ms = None
         if args.resident:
-            env.run(acts[:n1], n1, lanes=lanes, resident=True)
+            env.run(acts[:n1], n1, lanes=1, resident=True)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-            env.run(acts, args.steps, lanes=lanes, resident=True)
+            env.run(acts, args.steps, lanes=1, resident=True)
             e1.record(stream)
             torch.cuda.synchronize()
             resident_ms = e0.elapsed_time(e1) / args.steps
@@ -345,8 +345,8 @@ def main():
         if resident_ms is not None:
             line["resident_rollout"] = {
                 "ms_per_step": round(resident_ms, 5), "env_steps_per_s": round(N * 1e3 / resident_ms, 1),
-                "lanes": lanes,
-                "note": "the same K steps as ONE wg_rollout launch per walker range: state in registers across steps, "
+                "lanes": 1,
+                "note": "the same K steps as ONE wg_rollout launch: each wave's walker state in registers across steps, "
                         "per-step obs/reward/done/info written every step (open-loop actions known up front); not the "
                         "headline, which is one launch per env step (SURVEY 8(d))"}
         if tr:

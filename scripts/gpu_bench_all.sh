@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 t=${1:-r02}
 S=scripts/gpu_session.sh
-$S "${t}_bench_canonical:300:python bench.py" \
+$S "${t}_bench_canonical:300:python bench.py --resident" \
    "${t}_prof_canonical:300:rocprofv3 --kernel-trace --stats -d gpurun_out/${t}_prof_canonical -o run --output-format csv -- python bench.py --no-cpu-baseline" \
    "${t}_bench_ragged:400:python bench.py --workload ragged" \
    "${t}_prof_ragged:300:rocprofv3 --kernel-trace --stats -d gpurun_out/${t}_prof_ragged -o run --output-format csv -- python bench.py --workload ragged --no-cpu-baseline" \

@@ -2,14 +2,15 @@
 """Compile-time A/B of the step kernel (profiling aid, not product).
 
     python scripts/variant_ab.py build NAME=FLAGS ...     # here (CPU): build_ab/lib_NAME.so, e.g.
-                                                          #   base= soa0=-DWG_LEAN_SOA=0 abl1=-DWG_ABLATE=1
+                                                          #   base= slow=-DWG_FAST_SPRING=0 abl1=-DWG_ABLATE=1
     python scripts/variant_ab.py run [rounds] [workload] [NAME:ENV=V,ENV=V ...]
                                                           # GPU box: every .so in build_ab/ plus env variants of the
                                                           # in-tree library, interleaved rounds
 
 Each (variant, round) runs in its own process (WALKER_HIP_LIB picks the library) on the bench workload and
 reports the per-launch time with HIP events for one full-batch launch per step (lanes 1) and for bench.py's
-default walker ranges (lanes 2); the summary is the median over rounds.  Results are written to
+default walker ranges (lanes 2); the summary is the median over rounds.  WG_AB_RESIDENT=1 times run(resident=True)
+(one wg_rollout launch for all steps) instead.  Results are written to
 gpurun_out/variant_ab.json."""
 import json
 import os

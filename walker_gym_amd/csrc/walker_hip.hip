@@ -353,9 +353,7 @@ __device__ __forceinline__ void spring_edge(const EdgeRec &e, int le, int lm, fl
 
 // One incidence entry's spring term (float64) and damping force (float32), read from LDS.
 struct IncTerm { double t0, t1, t2; float f0, f1, f2; };
-// Spring-term storage of a tile in LDS.  TermsAoS: t[3 le + c] (float64), df[3 le + c] (float32) — the
-// workgroup kernel.  TermsSoA: three float64 planes and three float32 planes of `pl` entries — the lean
-// kernels: the edge lanes' stores are then consecutive (conflict-free) instead of a 24-B lane stride.
+// Spring-term storage of a tile in LDS, every kernel: t[3 le + c] (float64), df[3 le + c] (float32).
 struct TermsAoS {
     double *t;
     float *f;
@@ -365,18 +363,6 @@ struct TermsAoS {
     __device__ __forceinline__ void put(int le, double t0, double t1, double t2, float f0, float f1, float f2) const {
         t[3 * le] = t0; t[3 * le + 1] = t1; t[3 * le + 2] = t2;
         f[3 * le] = f0; f[3 * le + 1] = f1; f[3 * le + 2] = f2;
-    }
-};
-struct TermsSoA {
-    double *t;
-    float *f;
-    int pl;
-    __device__ __forceinline__ IncTerm get(int le) const {
-        return IncTerm{t[le], t[pl + le], t[2 * pl + le], f[le], f[pl + le], f[2 * pl + le]};
-    }
-    __device__ __forceinline__ void put(int le, double t0, double t1, double t2, float f0, float f1, float f2) const {
-        t[le] = t0; t[pl + le] = t1; t[2 * pl + le] = t2;
-        f[le] = f0; f[pl + le] = f1; f[2 * pl + le] = f2;
     }
 };
 template <class TS>
@@ -1162,7 +1148,7 @@ struct LeanGeo {
     int lgM;                                  // log2(M)
     int slice;                                // LDS bytes per wave
     int off_df, off_inc, off_x;               // byte offsets in the slice (spring terms at 0)
-    int pl;                                   // entries per spring-term plane (SoA; >= wpw * K, even)
+    int pl;                                   // spring-term slots of a wave tile (>= wpw * K, multiple of 4)
     float invK, invA, invM;                   // invM = 1/M, exact (M | 64 is a power of two)
 };
 
@@ -1310,19 +1296,10 @@ __device__ __forceinline__ LeanTile lean_tile_of(const wg_batch &b, const float 
     return t;
 }
 
-// Every global load of the wave's walkers, issued back to back.
-#ifndef WG_KARG_EARLY
-#define WG_KARG_EARLY 0
-#endif
-// Load order: 0 (default) pos, vel, spring records with their incidence words, mass-loop inputs, muscles;
-// 1 (A/B build) what the springs need first (pos, vel, the muscles' act inputs, the spring records), then what
-// only the mass loop needs, so the wait before the springs leaves the mass-loop loads in flight.  Measured
-// (scripts/variant_ab.py, 5 rounds, one box): 47.7 us per launch for 0, 48.5 for 1 — in steady state a wave
-// spends ~4K of its ~25K cycles on loads and the rest computing (scripts/stamps.py), so there is
-// little latency left to hide.
-#ifndef WG_LOAD_ORDER
-#define WG_LOAD_ORDER 0
-#endif
+// Every global load of the wave's walkers, issued back to back: pos, vel, spring records with their incidence
+// words, mass-loop inputs, muscles.  (Issuing what the springs need first and the mass-loop inputs last measured
+// 48.5 against 47.7 us per launch, profiles/r02_ab_loadorder_karg.json: in steady state a wave spends ~4K of its
+// ~25K cycles on loads, so there is little latency left to hide.)
 template <int NE>
 __device__ __forceinline__ void lean_load_mass(const wg_batch &b, const LeanTile &t, int lane, LeanIn<NE> &L) {
     const uint32_t pl = t.P0 + lane;
@@ -1361,23 +1338,15 @@ __device__ __forceinline__ void lean_load(const wg_batch &b, const KParams &kp, 
         L.p3[0] = gp[0]; L.p3[1] = gp[1]; L.p3[2] = gp[2];
         L.v3[0] = gv[0]; L.v3[1] = gv[1]; L.v3[2] = gv[2];
     }
-    if (WG_LOAD_ORDER) lean_load_muscles<NE>(b, kp, action, action_stride, t, lane, L);
     const uint32_t *incw = reinterpret_cast<const uint32_t *>(b.inc) + t.E0;   // 2 u16 entries per word
 #pragma unroll
     for (int it = 0; it < NE; it++) {
         const int le = lane + 64 * it;
         if (le < t.nE) L.er[it] = load_edge(b.edges, t.E0 + (uint32_t)le);
-        if (!WG_LOAD_ORDER && le < t.nE) L.gi[it] = incw[(uint32_t)le];
-    }
-    if (WG_LOAD_ORDER) {
-#pragma unroll
-        for (int it = 0; it < NE; it++) {
-            const int le = lane + 64 * it;
-            if (le < t.nE) L.gi[it] = incw[(uint32_t)le];
-        }
+        if (le < t.nE) L.gi[it] = incw[(uint32_t)le];
     }
     lean_load_mass<NE>(b, t, lane, L);
-    if (!WG_LOAD_ORDER) lean_load_muscles<NE>(b, kp, action, action_stride, t, lane, L);
+    lean_load_muscles<NE>(b, kp, action, action_stride, t, lane, L);
 }
 
 // double gathered from another lane (two ds_bpermute), all lanes taking part
@@ -1452,26 +1421,15 @@ __device__ __forceinline__ void pair_forces(const wg_batch &b, const KParams &kp
     }
 }
 
-// Spring-term layout of the lean kernels: interleaved (default) or planes (-DWG_LEAN_SOA=1, an A/B build).
-// Measured on the canonical bench (scripts/variant_ab.py, 5 interleaved rounds, one box): interleaved 47.3 us
-// per launch, planes 48.1 — the planes make the edge lanes' stores conflict-free, but the mass loop's random
-// reads then need three separate 8-B reads per term instead of one ds_read2_b64 + one ds_read_b64.
-#ifndef WG_LEAN_SOA
-#define WG_LEAN_SOA 0
-#endif
+// Spring terms of the lean kernels, interleaved per edge.  (Three f64 and three f32 planes make the edge lanes'
+// stores conflict-free, but the mass loop's random reads then take three separate 8-B reads per term instead of
+// one ds_read2_b64 + one ds_read_b64: 48.1 against 47.3 us per launch, profiles/r02_ab_soa_canonical.json.)
 
 
-#if WG_LEAN_SOA
-typedef TermsSoA LeanTerms;
-__device__ __forceinline__ LeanTerms lean_terms(char *sl, const LeanGeo &lg) {
-    return TermsSoA{reinterpret_cast<double *>(sl), reinterpret_cast<float *>(sl + lg.off_df), lg.pl};
-}
-#else
 typedef TermsAoS LeanTerms;
 __device__ __forceinline__ LeanTerms lean_terms(char *sl, const LeanGeo &lg) {
     return TermsAoS{reinterpret_cast<double *>(sl), reinterpret_cast<float *>(sl + lg.off_df)};
 }
-#endif
 
 // One wave's tile after its loads: the edge lanes leave the spring term t and the damping force df of every
 // edge in LDS, then each mass lane walks its incidence list, dividing by m as the reference does (mass_step).
@@ -1496,9 +1454,8 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
     const float mf = L.mf;
     const bool pin = L.pin != 0;
 
-    // ================= act (gym/optimized_walker.py:27-43,164-172); the incidence lists go to LDS after the
-    // springs (WG_LOAD_ORDER 1: their loads are still in flight while the springs run)
-    if (!WG_LOAD_ORDER && !RES) {   // (the resident kernel writes them once, before its first step)
+    // ================= act (gym/optimized_walker.py:27-43,164-172); the incidence lists go to LDS first
+    if (!RES) {   // (the resident kernel writes them once, before its first step)
 #pragma unroll
         for (int it = 0; it < NE; it++)
             if (lane + 64 * it < nE) s_inc[lane + 64 * it] = L.gi[it];
@@ -1558,11 +1515,6 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
         Gath g;
         gather(it, g);
         spring(it, g);
-    }
-    if (WG_LOAD_ORDER) {
-#pragma unroll
-        for (int it = 0; it < NE; it++)
-            if (lane + 64 * it < nE) s_inc[lane + 64 * it] = L.gi[it];
     }
     wave_sync();
     STAMP(3);
@@ -1688,11 +1640,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lean_waves(
     LeanGeo lg) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-#if WG_KARG_EARLY
-    // experiment: every pointer the tile loads from in SGPRs at entry (one kernarg wait instead of several)
-    asm volatile("" ::"s"(b.pos), "s"(b.vel), "s"(b.edges), "s"(b.inc), "s"(b.inc_off), "s"(b.mass),
-                 "s"(b.muscle_x), "s"(b.muscle_bounds), "s"(b.steps), "s"(action), "s"(b.M), "s"(b.K), "s"(b.A));
-#endif
     const int tile = blockIdx.x * lg.wpb + wv;
     if (tile * lg.wpw >= b.N) return;
 #ifdef WG_STAMPS
@@ -2232,7 +2179,7 @@ bool lean_geo(const wg_batch *b, int obs_stride, LeanGeo *out, int spring_mode =
     const int wpb = env_int("WG_LEAN_WAVES", 4);
     g.wpb = (wpb == 1 || wpb == 2) ? wpb : 4;
     const int ew = g.wpw * b->K;                          // springs of a full wave tile
-    g.pl = (ew + 3) & ~3;                                 // plane length: 16-B aligned f64 and f32 planes
+    g.pl = (ew + 3) & ~3;                                 // spring-term slots: 16-B aligned regions
     // t (f64 x3) | df (f32 x3) | incidence words | x (observation rows go from registers to HBM, no LDS tile)
     g.off_df = align16(g.pl * 24);
     g.off_inc = g.off_df + align16(g.pl * 12);

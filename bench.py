@@ -44,7 +44,7 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--walkers", type=int, default=65536, help="walkers per GPU")
-    ap.add_argument("--workload", default="canonical", choices=["canonical", "balance", "ragged", "chain"])
+    ap.add_argument("--workload", default="canonical", choices=["canonical", "balance", "ragged", "chain", "lattice25"])
     ap.add_argument("--chain-points", type=int, default=100, help="masses per chain walker (--workload chain)")
     ap.add_argument("--lanes", type=int, default=None, help="walker ranges on separate streams (default: auto)")
     ap.add_argument("--resident", action="store_true", help="also time the K steps as ONE wg_rollout launch (state in "
@@ -111,6 +111,8 @@ def make_spec(workload: str, n: int, seed: int, chain_points: int = 100):
         return balance_spec(n), dict(in3d=0)
     if workload == "chain":
         return chain_walkers(n, chain_points, seed=seed), dict(in3d=1, g=0.0, ground=-1.0e6, pair_mode=1)
+    if workload == "lattice25":
+        return canonical_walkers(n, seed=seed, M=25, K=60, A=10), dict(in3d=1)
     return ragged_walkers(n, seed=seed, mmin=4, mmax=32), dict(in3d=1)
 
 
@@ -121,7 +123,9 @@ DATA = {"canonical": "synthetic (seeded; SURVEY §8(d) canonical walker M=16, K=
         "ragged": "synthetic (seeded mixed topologies, M ~ U{4..32}, K ~ U{M..2M}, A = K // 5; U(-1,1) actions, "
                   "distinct per step)",
         "chain": "synthetic (performance_demo chain: U(-100,100) positions, U(-10,10) velocities, Skeleton(k=50) "
-                 "links, per-walker Point.gravity; no muscles)"}
+                 "links, per-walker Point.gravity; no muscles)",
+        "lattice25": "synthetic (seeded uniform 5x5-lattice walkers, M=25 (not a divisor of 64), K=60, A=10; U(-1,1) "
+                     "actions, distinct per step)"}
 
 
 def bytes_per_walker_step(host, in3d: bool) -> float:

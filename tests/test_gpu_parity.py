@@ -201,6 +201,33 @@ def test_size_extremes_vs_oracle(case):
     _oracle_compare(spec, dict(in3d=1), 8, acts)
 
 
+def test_uniform_non_divisor_M_on_wave_kernel():
+    """A uniform batch whose M does not divide 64 (5x5 lattice, M = 25) is stepped as wave tiles of whole walkers
+    (the barrier-free wave kernel, identity order): oracle parity, and bitwise equal to the workgroup kernel
+    (WG_UNIFORM_WAVES=0, read when the device batch is built)."""
+    import torch
+    from walker_gym_amd.batched_env import BatchedPhysicsEnv
+    from walker_gym_amd.synthetic import canonical_walkers
+    N = 3000
+    spec = canonical_walkers(N, seed=31, M=25, K=60, A=10)
+    acts = np.random.default_rng(31).uniform(-1, 1, (12, N, 10)).astype(np.float32)
+    env, _ = _oracle_compare(spec, dict(in3d=1), 12, acts)
+    assert env.batch.ragged_kind == 2 and env.batch.row is None
+    outs = []
+    for flag in ("1", "0"):
+        os.environ["WG_UNIFORM_WAVES"] = flag
+        try:
+            e = BatchedPhysicsEnv(spec, in3d=1)
+        finally:
+            del os.environ["WG_UNIFORM_WAVES"]
+        assert e.batch.ragged_kind == (2 if flag == "1" else 0)
+        o, r, d = e.rollout(acts, resident=False)
+        torch.cuda.synchronize()
+        outs.append([o.cpu().numpy(), r.cpu().numpy(), e.pos.cpu().numpy(), e.vel.cpu().numpy()])
+    for x, y in zip(*outs):
+        assert np.array_equal(x.view(np.uint8), y.view(np.uint8))
+
+
 def _tiny_walkers(N, seed):
     """Walkers of 1-3 masses: single free masses (no spring), pairs with one spring, triangles; some with no
     muscle.  Exercises the smallest tiles of the workgroup kernel."""

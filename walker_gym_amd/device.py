@@ -4,6 +4,7 @@ torch.distributed); all per-step compute is the HIP kernel."""
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import Optional
 
 import numpy as np
@@ -73,8 +74,14 @@ class DeviceBatch:
         self.plan = None
         self.plan_blocks = 0
         self.ragged_kind = 0
+        L = _lib.load()
+        lean_shape = 4 <= self.M <= 64 and 64 % self.M == 0
+        if (not self.ragged and not lean_shape and self.A <= 64 and L.wg_wave_edge_passes(self.M, self.K) > 0
+                and os.environ.get("WG_UNIFORM_WAVES", "1") != "0"):
+            # a uniform batch the lean kernel does not take (M not dividing 64): stepped as wave tiles of whole
+            # walkers (the barrier-free wave kernel; identity order) instead of workgroup tiles
+            self.ragged = True
         if self.ragged:
-            L = _lib.load()
             plan = np.zeros(self.N + 1, np.int32)
             args = (host.mass_off.ctypes.data_as(C.c_void_p), host.edge_off.ctypes.data_as(C.c_void_p),
                     host.muscle_off.ctypes.data_as(C.c_void_p), self.N, plan.ctypes.data_as(C.c_void_p), self.N + 1)

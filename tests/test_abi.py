@@ -137,6 +137,24 @@ def test_launch_geometry_canonical(lib):
     assert info.lds_bytes <= 32768   # five workgroups per CU (160 KiB LDS)
 
 
+def test_launch_geometry_wide_workgroups(lib, monkeypatch):
+    """M > 64: the workgroup size in 256..512 threads that leaves the fewest idle lanes (walker_hip.hip
+    uniform_geo), halved back while the grid has fewer than 512 workgroups; WG_WIDE=0 keeps 256."""
+    def geo(N, M, K):
+        b = _lib.WgBatch(N=N, M=M, K=K, A=0, ragged=0)
+        for f in ("pos", "vel", "acc", "mass", "edges", "inc", "inc_off", "muscle_x", "steps"):
+            setattr(b, f, 16)
+        info = _lib.WgLaunchInfo()
+        assert lib.wg_launch_geometry(C.byref(b), C.byref(info)) == 0
+        return info.threads, info.walkers_per_block
+    assert geo(4096, 100, 99) == (512, 5)      # the performance_demo chain: 500 of 512 lanes busy
+    assert geo(4096, 200, 199) == (448, 2)
+    assert geo(4096, 128, 127) == (256, 2)
+    assert geo(40, 100, 99) == (128, 1)        # small batch: more, smaller workgroups
+    monkeypatch.setenv("WG_WIDE", "0")
+    assert geo(4096, 100, 99) == (256, 2)
+
+
 def test_wave_edge_passes(lib):
     """Spring passes of a wave tile (walker_hip.hip wave_passes): enough for the longest walker and for 64 masses of
     the densest one, rounded to an instantiated count; 0 = the batch cannot use the wave kernel."""

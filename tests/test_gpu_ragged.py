@@ -81,7 +81,7 @@ def test_wave_kernel_vs_oracle_caller_order():
     assert np.array_equal(env.muscle_x.cpu().numpy(), orc.mx)
 
 
-@pytest.mark.parametrize("case", ["ragged", "uniform_M13", "uniform_M100"])
+@pytest.mark.parametrize("case", ["ragged", "uniform_M13", "uniform_M100", "uniform_M100_wide"])
 def test_pair_forces_workgroup_kernel_vs_oracle(case):
     import torch
     from oracle.oracle import Oracle
@@ -93,8 +93,10 @@ def test_pair_forces_workgroup_kernel_vs_oracle(case):
         spec = ragged_walkers(600, seed=7, mmin=3, mmax=40)
     elif case == "uniform_M13":
         spec = topology_spec("insect", 500, 1)
-    else:
+    elif case == "uniform_M100":
         spec = canonical_walkers(40, seed=7, M=100, K=180, A=10)
+    else:   # enough walkers for 512-thread workgroups of 5 walkers (wg_launch_geometry checked below)
+        spec = canonical_walkers(2600, seed=8, M=100, K=180, A=10)
     P = int(spec["mass_off"][-1])
     spec["charge"] = rng.uniform(-3, 3, P)
     spec["radius"] = rng.uniform(0.5, 2.0, P)
@@ -102,9 +104,13 @@ def test_pair_forces_workgroup_kernel_vs_oracle(case):
     A = max(1, int(np.max(spec["n_muscles"])))
     params = dict(in3d=1, pair_mode=7, pair_g=500.0, pair_k=2.0e3, bounce_k=400.0)
     env = BatchedPhysicsEnv(spec, device="cuda:0", **params)
+    if case == "uniform_M100_wide":
+        info = env.launch_geometry()
+        assert info["threads"] == 512 and info["walkers_per_block"] == 5, info
     orc = Oracle(spec, params)
-    acts = rng.uniform(-1, 1, (10, N, A)).astype(np.float32)
-    for t in range(10):
+    T = 4 if case == "uniform_M100_wide" else 10
+    acts = rng.uniform(-1, 1, (T, N, A)).astype(np.float32)
+    for t in range(T):
         obs, rew, done, info = env.step(acts[t])
         ref = orc.step(acts[t])
     torch.cuda.synchronize()

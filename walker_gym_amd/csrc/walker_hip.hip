@@ -51,7 +51,7 @@ constexpr int EPL = 4;               // edges per lane per pass held in register
 #define WG_NTHREADS 256
 #endif
 constexpr int NTHREADS = WG_NTHREADS;   // default workgroup size (walkers fill 256 mass lanes)
-constexpr int MAXT = 256;               // __launch_bounds__: workgroups are 64..256 threads
+constexpr int MAXT = 512;               // __launch_bounds__: workgroups are 64..512 threads (> 256: M > 64 only)
 #ifndef WG_ABLATE
 #define WG_ABLATE 0   // profiling builds only (scripts/variant_ab.py): bit k skips phase k; 0 in the product
 #endif
@@ -256,6 +256,29 @@ __device__ inline double ddiv_f32d(double a, double b, double y) {
     const double am = __builtin_fabs(m);
     if (__builtin_expect(am >= 0x1p-800 && am <= 0x1p800, 1)) return m;
     return a == 0.0 ? q : a / b;
+}
+
+// 1/d for a double d = (double)cur, cur a normal float: v_rcp_f64 and two Newton steps, within about
+// one ulp of 1/d (not necessarily RN64(1/d)).  That suffices for the Markstein correction in
+// ddiv_fast / fdiv_fast to return the correctly rounded quotient of the spring: a quotient X/cur of two
+// 24-bit floats lies at least 2^-78 (relative) from every double rounding midpoint and 2^-49 from every
+// float one, while the corrected value is within ~2^-100 of X/cur (tests/test_exact_division.py runs
+// the same construction on the host).
+__device__ __forceinline__ double rcp64_nr(double d) {
+    double y = __builtin_amdgcn_rcp(d);
+    double e = __builtin_fma(-d, y, 1.0);
+    y = __builtin_fma(y, e, y);
+    e = __builtin_fma(-d, y, 1.0);
+    return __builtin_fma(y, e, y);
+}
+
+// sqrtf of a float s in [2^-96, 2^126): v_sqrt_f32 and the one-ulp correction, the same steps as the compiler's
+// correctly rounded sqrtf minus its small-input rescaling and zero/inf fix-up, which this range never needs
+__device__ __forceinline__ float sqrt_mid(float s) {
+    const float r = __builtin_amdgcn_sqrtf(s);
+    const float rd = __uint_as_float(__float_as_uint(r) - 1u), ru = __uint_as_float(__float_as_uint(r) + 1u);
+    float o = (__builtin_fmaf(-rd, r, s) <= 0.f) ? rd : r;
+    return (__builtin_fmaf(-ru, r, s) > 0.f) ? ru : o;
 }
 
 // Global -> LDS copy of n 4-byte words (16-B vector loads when both ends allow it).
@@ -663,6 +686,40 @@ __device__ __forceinline__ void pair_central_term(double coef, double slo, doubl
     ay = (float)((double)ay + ddiv_f32d(t1, md, ym));
     az = (float)((double)az + ddiv_f32d(t2, md, ym));
 }
+#ifndef WG_FAST_PAIR
+#define WG_FAST_PAIR 1
+#endif
+// a / b by Markstein's correction from y ~ 1/b, written -(-r*y - q) so that a = +-0 gives the IEEE signed zero
+__device__ __forceinline__ double mk_div(double a, double b, double y) {
+    const double q = a * y;
+    const double r = __builtin_fma(-q, b, a);
+    return -__builtin_fma(-r, y, -q);
+}
+// pair_central_term without IEEE divisions or the compiler's sqrtf: the correctly rounded sqrt of a float in
+// [2^-96, 2^126) (sqrt_mid); f / r^2 from rcp64_nr(r^2) and Markstein's step (the compiler's own double division
+// minus the operand scaling, which no operand in the range admitted here needs); RN64(1/r) as one Newton step
+// from r * y2 (r is a float32 value: 1/r lies >= 2^-77 (relative) from every double rounding midpoint, the
+// step lands within ~2^-100); the divisions by r and m as ddiv_f32d's Markstein quotients.  bad is raised for
+// a distance outside that range or |f| < 2^-600 (zero included: every later numerator is then >= 2^-812 in
+// magnitude or exactly zero, so no residual underflows); a non-finite quotient makes the sum non-finite.  The
+// caller redoes the partner loop with pair_central_term when bad is set or the sum is not finite.
+__device__ __forceinline__ void pair_central_fast(double coef, double slo, double shi, float d0, float d1, float d2,
+                                                  double md, double ym, float &ax, float &ay, float &az, bool &bad) {
+    const float sq = (float)(((double)(d0 * d0) + (double)(d1 * d1)) + (double)(d2 * d2));   // np_norm3's sum
+    const double r = (double)sqrt_mid(sq);             // >= 2^-48 > Config.r: max(distance, r) is the distance
+    const double r2 = r * r;
+    const double y2 = rcp64_nr(r2);
+    const double f = mk_div(((-coef) * slo) * shi, r2, y2);
+    const double yr0 = r * y2;
+    const double yr = __builtin_fma(yr0, __builtin_fma(-r, yr0, 1.0), yr0);
+    const double nf = -f;
+    ax = (float)((double)ax + mk_div(mk_div(nf * (double)d0, r, yr), md, ym));
+    ay = (float)((double)ay + mk_div(mk_div(nf * (double)d1, r, yr), md, ym));
+    az = (float)((double)az + mk_div(mk_div(nf * (double)d2, r, yr), md, ym));
+    const uint32_t fe = ((uint32_t)__double2hiint(f) >> 20) & 0x7ffu;
+    bad = bad || !(sq >= 0x1p-96f && sq < 0x1p126f) || fe < 1023u - 600u;
+}
+
 // One colliding bounce partner: resilience(i, r_s + r_i, k/2) seen from this end (gym/engine.py:78-102), the
 // float64 force path with the float32 numerator nf * d.
 __device__ __forceinline__ void bounce_term(float cur, float nf, float d0, float d1, float d2, double md, double ym,
@@ -695,12 +752,32 @@ __device__ void pair_forces_lds(const wg_batch &b, const KParams &kp, const floa
         if (!(kp.pair_mode & (1 << pass))) continue;
         const double coef = pass == 0 ? kp.pair_g : kp.pair_k;
         const double sq = pass == 0 ? md : (b.charge ? b.charge[g0 + q] : kp.pair_e);
-        for (int pj = 0; pj < M; pj++) {
-            if (pj == q) continue;
+        auto partner = [&](int pj, double &os, float &d0, float &d1, float &d2) {
             const float *o3 = spos + 3 * (lm + pj);
-            const double os = pass == 0 ? (double)sm[lm + pj] : (b.charge ? b.charge[g0 + pj] : kp.pair_e);
-            const float d0 = o3[0] - p3[0], d1 = o3[1] - p3[1], d2 = o3[2] - p3[2];   // partner - self
-            pair_central_term(coef, pj < q ? os : sq, pj < q ? sq : os, d0, d1, d2, md, ym, ax, ay, az);
+            os = pass == 0 ? (double)sm[lm + pj] : (b.charge ? b.charge[g0 + pj] : kp.pair_e);
+            d0 = o3[0] - p3[0]; d1 = o3[1] - p3[1]; d2 = o3[2] - p3[2];   // partner - self
+        };
+        const float sx = ax, sy = ay, sz = az;
+        bool bad = !WG_FAST_PAIR;
+        if (WG_FAST_PAIR) {
+            for (int pj = 0; pj < M; pj++) {
+                if (pj == q) continue;
+                double os;
+                float d0, d1, d2;
+                partner(pj, os, d0, d1, d2);
+                pair_central_fast(coef, pj < q ? os : sq, pj < q ? sq : os, d0, d1, d2, md, ym, ax, ay, az, bad);
+            }
+            bad = bad || !__builtin_isfinite(ax + ay + az);
+        }
+        if (__builtin_expect(bad, 0)) {   // the exact pass: IEEE divisions and sqrtf
+            ax = sx; ay = sy; az = sz;
+            for (int pj = 0; pj < M; pj++) {
+                if (pj == q) continue;
+                double os;
+                float d0, d1, d2;
+                partner(pj, os, d0, d1, d2);
+                pair_central_term(coef, pj < q ? os : sq, pj < q ? sq : os, d0, d1, d2, md, ym, ax, ay, az);
+            }
         }
     }
     if (kp.pair_mode & 4) {                  // gym/engine.py:114-125, partners j < q, then j != q, then j > q
@@ -1160,19 +1237,6 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// 1/d for a double d = (double)cur, cur a normal float: v_rcp_f64 and two Newton steps, within about
-// one ulp of 1/d (not necessarily RN64(1/d)).  That suffices for the Markstein correction in
-// ddiv_fast / fdiv_fast to return the correctly rounded quotient of the spring: a quotient X/cur of two
-// 24-bit floats lies at least 2^-78 (relative) from every double rounding midpoint and 2^-49 from every
-// float one, while the corrected value is within ~2^-100 of X/cur (tests/test_exact_division.py runs
-// the same construction on the host).
-__device__ __forceinline__ double rcp64_nr(double d) {
-    double y = __builtin_amdgcn_rcp(d);
-    double e = __builtin_fma(-d, y, 1.0);
-    y = __builtin_fma(y, e, y);
-    e = __builtin_fma(-d, y, 1.0);
-    return __builtin_fma(y, e, y);
-}
 
 // Gather a float from another lane of the wave (ds_bpermute: LDS crossbar, no LDS allocation).  Executed
 // by every lane (convergent): a lane that is inactive as a SOURCE would read back as 0.
@@ -1204,14 +1268,6 @@ __device__ __forceinline__ void spring_terms_cold(const EdgeRec &e, float x, flo
     }
 }
 
-// sqrtf of a float s in [2^-96, 2^126): v_sqrt_f32 and the one-ulp correction, the same steps as the compiler's
-// correctly rounded sqrtf minus its small-input rescaling and zero/inf fix-up, which this range never needs
-__device__ __forceinline__ float sqrt_mid(float s) {
-    const float r = __builtin_amdgcn_sqrtf(s);
-    const float rd = __uint_as_float(__float_as_uint(r) - 1u), ru = __uint_as_float(__float_as_uint(r) + 1u);
-    float o = (__builtin_fmaf(-rd, r, s) <= 0.f) ? rd : r;
-    return (__builtin_fmaf(-ru, r, s) > 0.f) ? ru : o;
-}
 
 __device__ __forceinline__ void spring_terms(const EdgeRec &e, float x, float pix, float piy, float piz, float pjx,
                                              float pjy, float pjz, float vix, float viy, float viz, float vjx,
@@ -1366,13 +1422,31 @@ __device__ __forceinline__ void pair_central(double coef, double sq, const float
                                              bool is_mass, float &ax, float &ay, float &az) {
     const int gb = lane & ~(M - 1), q = lane & (M - 1);
     const double md = (double)mf, ym = 1.0 / md;
-    for (int pj = 0; pj < M; pj++) {
-        const int src = (gb + pj) << 2;
-        const float ox = lane_gather(p3[0], src), oy = lane_gather(p3[1], src), oz = lane_gather(p3[2], src);
-        const double os = lane_gather_d(sq, src);
-        if (!is_mass || pj == q) continue;
-        const float d0 = ox - p3[0], d1 = oy - p3[1], d2 = oz - p3[2];   // partner - self
-        pair_central_term(coef, pj < q ? os : sq, pj < q ? sq : os, d0, d1, d2, md, ym, ax, ay, az);
+    const float sx = ax, sy = ay, sz = az;
+    bool bad = !WG_FAST_PAIR && is_mass;
+    if (WG_FAST_PAIR) {
+        for (int pj = 0; pj < M; pj++) {
+            const int src = (gb + pj) << 2;
+            const float ox = lane_gather(p3[0], src), oy = lane_gather(p3[1], src), oz = lane_gather(p3[2], src);
+            const double os = lane_gather_d(sq, src);
+            if (!is_mass || pj == q) continue;
+            const float d0 = ox - p3[0], d1 = oy - p3[1], d2 = oz - p3[2];   // partner - self
+            pair_central_fast(coef, pj < q ? os : sq, pj < q ? sq : os, d0, d1, d2, md, ym, ax, ay, az, bad);
+        }
+        bad = is_mass && (bad || !__builtin_isfinite(ax + ay + az));
+    }
+    // the exact pass (IEEE divisions and sqrtf) for the lanes that need it; every lane gathers (wave-uniform branch)
+    if (__builtin_expect(__ballot(bad) != 0, 0)) {
+        float cx = sx, cy = sy, cz = sz;
+        for (int pj = 0; pj < M; pj++) {
+            const int src = (gb + pj) << 2;
+            const float ox = lane_gather(p3[0], src), oy = lane_gather(p3[1], src), oz = lane_gather(p3[2], src);
+            const double os = lane_gather_d(sq, src);
+            if (!bad || pj == q) continue;
+            const float d0 = ox - p3[0], d1 = oy - p3[1], d2 = oz - p3[2];
+            pair_central_term(coef, pj < q ? os : sq, pj < q ? sq : os, d0, d1, d2, md, ym, cx, cy, cz);
+        }
+        if (bad) { ax = cx; ay = cy; az = cz; }
     }
 }
 
@@ -2084,7 +2158,16 @@ Geo uniform_geo(const wg_batch *b, int obs_stride, bool no_lite = false) {
     // walkers per workgroup: fill the 256 mass lanes, keep edges within EPL registers per lane,
     // and make sure the grid has >= 512 workgroups when the batch allows it.
     int W = std::max(1, NTHREADS / b->M);
-    if (b->K > 0) W = std::max(1, std::min(W, EPL * NTHREADS / std::max(1, b->K)));
+    if (b->M > 64 && env_int("WG_WIDE", 1)) {
+        // M > 64: the workgroup size (256..512 threads) that leaves the fewest idle lanes; 100-mass chains run
+        // 5 walkers on 512 threads (98 % of the lanes busy) instead of 2 on 256 (78 %)
+        int best = 0, bestT = NTHREADS;
+        for (int T = NTHREADS; T <= MAXT; T += 64) {
+            const int w = T / b->M;
+            if (w >= 1 && (int64_t)w * b->M * bestT > (int64_t)best * T) { best = w * b->M; bestT = T; W = w; }
+        }
+    }
+    if (b->K > 0) W = std::max(1, std::min(W, EPL * MAXT / std::max(1, b->K)));
     while (W > 1 && (b->N + W - 1) / W < 512) W = std::max(1, W / 2);
     g.W = W;
     const bool shfl_shape = b->M <= 64 && (64 % b->M) == 0 && !(WG_ABLATE & 64);

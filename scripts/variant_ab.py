@@ -61,7 +61,8 @@ def time_one(lib, workload, steps=200, warm=20):
 
 
 def run(rounds, workload, env_specs=()):
-    variants = [(f[4:-3], os.path.join(OUT, f), {}) for f in sorted(os.listdir(OUT)) if f.endswith(".so")]
+    variants = [(f[4:-3], os.path.join(OUT, f), {}) for f in sorted(os.listdir(OUT)) if f.endswith(".so")] \
+        if os.path.isdir(OUT) else []
     lib = os.path.join(ROOT, "walker_gym_amd", "libwalker_hip.so")
     for spec in env_specs:
         name, _, kv = spec.partition(":")

@@ -32,7 +32,9 @@ acts = (torch.rand((60, N, max(1, env.batch.A)), device="cuda:0") * 2 - 1).conti
 env.run(acts[:50].contiguous(), 50, lanes=1)          # past the free fall, as in the bench's timed region
 env.run(acts[50:51].contiguous(), 1, lanes=1)
 torch.cuda.synchronize()
-W = env.batch.plan_blocks if env.batch.ragged else N * env.batch.M // 64   # waves (one tile each)
+geo = env.batch.launch_geometry()
+wpw = geo["walkers_per_block"] // max(1, geo["threads"] // 64)   # walkers per wave tile (lean kernel)
+W = env.batch.plan_blocks if env.batch.ragged else -(-N // wpw)     # waves (one tile each)
 st = np.zeros((W, 8), np.uint64)
 print("WG_LEAN_WAVES", os.environ.get("WG_LEAN_WAVES", "4"))
 L = _lib.load()

@@ -41,7 +41,7 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--steps", type=int, default=1000)   # time 1,000 steps after 50
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--walkers", type=int, default=65536, help="walkers per GPU")
     ap.add_argument("--workload", default="canonical", choices=["canonical", "balance", "ragged", "chain", "lattice25"])

@@ -137,6 +137,19 @@ def test_launch_geometry_canonical(lib):
     assert info.lds_bytes <= 32768   # five workgroups per CU (160 KiB LDS)
 
 
+def test_launch_geometry_wave_tiles(lib):
+    """ragged = 2 (sorted wave tiles): the wave kernel's geometry, 4 waves per workgroup and its LDS slices; the tile
+    count comes from the plan, so blocks and walkers per block are -1."""
+    b = _lib.WgBatch(N=1000, M=32, K=64, A=12, ragged=2)
+    for f in ("pos", "vel", "acc", "mass", "edges", "inc", "inc_off", "muscle_x", "steps", "mass_off", "edge_off",
+              "muscle_off"):
+        setattr(b, f, 16)
+    info = _lib.WgLaunchInfo()
+    assert lib.wg_launch_geometry(C.byref(b), C.byref(info)) == 0
+    assert info.threads == 256 and info.walkers_per_block == -1 and info.blocks == -1
+    assert 4 * 5 * 1024 <= info.lds_bytes <= 4 * 7 * 1024   # ~5.9 KB per wave at 2 spring passes
+
+
 def test_launch_geometry_wide_workgroups(lib, monkeypatch):
     """M > 64: the workgroup size in 256..512 threads that leaves the fewest idle lanes (walker_hip.hip
     uniform_geo), halved back while the grid has fewer than 512 workgroups; WG_WIDE=0 keeps 256."""

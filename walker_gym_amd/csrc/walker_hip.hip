@@ -2572,6 +2572,14 @@ int wg_launch_geometry(const wg_batch *b, wg_launch_info *info) {
         info->lds_bytes = lg.wpb * lg.slice;
         return 0;
     }
+    RagGeo rg{};
+    if (b->ragged == 2 && lean_enabled() && rag_geo(b, 0, &rg)) {   // the wave kernel: one tile per wave
+        info->threads = 64 * rg.wpb;
+        info->walkers_per_block = -1;   // tiles hold whole walkers up to 64 masses: the plan decides
+        info->blocks = -1;              // ceil(tiles / waves per workgroup), tiles from wg_plan_waves
+        info->lds_bytes = rg.wpb * rg.slice;
+        return 0;
+    }
     const Geo g = b->ragged ? ragged_geo(b) : uniform_geo(b, 0);
     info->threads = g.threads;
     info->walkers_per_block = g.W;

@@ -173,9 +173,16 @@ class DeviceBatch:
     def launch_geometry(self) -> dict:
         info = _lib.WgLaunchInfo()
         _lib.check(_lib.load().wg_launch_geometry(C.byref(self.struct), C.byref(info)), "wg_launch_geometry")
-        blocks = self.plan_blocks if self.ragged else info.blocks
-        return dict(threads=info.threads, walkers_per_block=info.walkers_per_block, blocks=blocks,
-                    lds_bytes=info.lds_bytes)
+        # ragged batches: the plan's blocks (workgroup kernel) or wave tiles (wave kernel, waves per workgroup)
+        blocks = info.blocks
+        if self.ragged:
+            wpb = max(1, info.threads // 64)
+            blocks = -(-self.plan_blocks // wpb) if self.ragged_kind == 2 else self.plan_blocks
+        geo = dict(threads=info.threads, walkers_per_block=info.walkers_per_block, blocks=blocks,
+                   lds_bytes=info.lds_bytes)
+        if self.ragged_kind == 2:
+            geo["wave_tiles"] = self.plan_blocks
+        return geo
 
     def state_dict(self) -> dict:
         sd = {k: getattr(self, k).clone() for k in self.STATE}

@@ -331,10 +331,13 @@ def main():
                          "traffic": (tr["hbm_bytes_per_launch"] if tr else None),
                          "bytes_per_walker_step": round(B, 1), "layout_bytes_per_walker_step": B_layout,
                          "kernel_ms_per_launch": round(head_ms, 5),
-                         "note": "achieved = N * B / the per-launch time of ONE full-batch launch per step (HIP "
-                                 "events on the launching stream; in a rocprofv3 --kernel-trace of this command "
-                                 "these are the full-grid launches, scripts/trace_kernels.py); B = SURVEY §8(d) "
-                                 "algorithmic bytes averaged over the walkers"},
+                         "note": ("achieved = N * B / the per-launch time of ONE full-batch launch per step (HIP "
+                                  "events on the launching stream; in a rocprofv3 --kernel-trace of this command "
+                                  "these are the full-grid launches, scripts/trace_kernels.py); B = SURVEY §8(d) "
+                                  "algorithmic bytes averaged over the walkers") if single_ms is not None else
+                                 (f"achieved = N * B / the time per step of the {lanes} walker ranges (--no-control: "
+                                  "no single-launch timing); B = SURVEY §8(d) algorithmic bytes averaged over the "
+                                  "walkers")},
         }
         if lanes > 1 or graph is not None:
             a2 = B * N / (step_ms * 1e-3) / 1e9

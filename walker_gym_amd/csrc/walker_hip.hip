@@ -1813,7 +1813,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
     wg_batch b, KParams kp, const float *__restrict__ action, int action_cols, int action_stride, wg_outputs o,
     const int32_t *__restrict__ plan, int ntiles, RagGeo rg) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    // the wave index as a wave-uniform (scalar) value: the plan entries and the tile's bases are then scalar loads
+    // (scalar cache, lgkmcnt) rather than vector loads each waited for before the next one can be addressed
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int tile = blockIdx.x * rg.wpb + wv;
     if (tile >= ntiles) return;
 #ifdef WG_STAMPS
@@ -1837,39 +1839,46 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
     const int w0 = plan[tile], w1 = plan[tile + 1], nw = w1 - w0;
     const int P0 = b.mass_off[w0], E0 = b.edge_off[w0], U0 = b.muscle_off[w0];
     const int nP = b.mass_off[w1] - P0, nE = b.edge_off[w1] - E0, nU = b.muscle_off[w1] - U0;
-    int wmo = 0, weo = 0, wuo = 0, wrow = 0, wsteps = 0;
-    if (lane <= nw) {
-        wmo = b.mass_off[w0 + lane] - P0; weo = b.edge_off[w0 + lane] - E0; wuo = b.muscle_off[w0 + lane] - U0;
-    }
-    if (lane < nw) { wrow = caller_row(b, w0 + lane); wsteps = b.steps[w0 + lane]; }
+    // every vector load that needs only the tile's bases, issued back to back from clamped (valid) indices: a load
+    // under a per-lane branch whose result the register allocator copies waits right there, and with vmcnt counting
+    // in order that wait covers every load before it.  Lanes past the tile's walkers / masses / springs / muscles
+    // load a duplicate and are given the reference values (zeros) once everything has landed.
     const bool is_mass = lane < nP, is_mus = lane < nU;
-    float p3[3] = {0.f, 0.f, 0.f}, v3[3] = {0.f, 0.f, 0.f};
-    float mf = 0.f;
-    int pin = 0;
-    if (is_mass) {
-        const float *gp = b.pos + 3 * (size_t)(P0 + lane), *gv = b.vel + 3 * (size_t)(P0 + lane);
+    const int lw = min(lane, nw), lr = min(lane, nw - 1);
+    int wmo = b.mass_off[w0 + lw] - P0, weo = b.edge_off[w0 + lw] - E0, wuo = b.muscle_off[w0 + lw] - U0;
+    int wsteps = b.steps[w0 + lr];
+    const int lp = P0 + min(lane, max(nP, 1) - 1);   // a tile has at least one mass
+    float p3[3], v3[3];
+    {
+        const float *gp = b.pos + 3 * (size_t)lp, *gv = b.vel + 3 * (size_t)lp;
         p3[0] = gp[0]; p3[1] = gp[1]; p3[2] = gp[2];
         v3[0] = gv[0]; v3[1] = gv[1]; v3[2] = gv[2];
-        mf = b.mass[P0 + lane];
-        if (b.pinned) pin = b.pinned[P0 + lane];
     }
+    float mf = b.mass[lp];
     EdgeRec er[NE];
     uint32_t gi[NE];
-    const uint32_t *incw = reinterpret_cast<const uint32_t *>(b.inc) + E0;
+    if (nE > 0) {
+        const uint32_t *incw = reinterpret_cast<const uint32_t *>(b.inc) + E0;
 #pragma unroll
-    for (int it = 0; it < NE; it++) {
-        const int le = lane + 64 * it;
-        if (le < nE) { er[it] = load_edge(b.edges, E0 + le); gi[it] = incw[le]; }
-    }
-    float mx = 0.f, mlo = 0.f, mhi = 0.f, mst = 0.f;
-    if (is_mus) {
-        mx = b.muscle_x[U0 + lane];
-        if (action) {
-            const float2 bd = reinterpret_cast<const float2 *>(b.muscle_bounds)[U0 + lane];
-            mlo = bd.x; mhi = bd.y;
-            if (kp.action_mode == 1) mst = b.muscle_stride[U0 + lane];
+        for (int it = 0; it < NE; it++) {
+            const int le = min(lane + 64 * it, nE - 1);
+            er[it] = load_edge(b.edges, E0 + le);
+            gi[it] = incw[le];
         }
     }
+    float mx = 0.f, mlo = 0.f, mhi = 0.f, mst = 0.f;
+    if (nU > 0) {
+        const int lu = U0 + min(lane, nU - 1);
+        mx = b.muscle_x[lu];
+        if (action) {
+            const float2 bd = reinterpret_cast<const float2 *>(b.muscle_bounds)[lu];
+            mlo = bd.x; mhi = bd.y;
+            if (kp.action_mode == 1) mst = b.muscle_stride[lu];
+        }
+    }
+    int wrow = w0 + lr, pin = 0;
+    if (b.row) wrow = b.row[w0 + lr];
+    if (b.pinned) pin = b.pinned[lp];
     // lane -> walker maps (tile-local offsets in LDS)
     if (lane <= nw) { s_mo[lane] = wmo; s_eo[lane] = weo; s_uo[lane] = wuo; }
     if (lane < nw) s_row[lane] = wrow;
@@ -1890,15 +1899,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
     if (!is_mus) uw = 0;
     wave_sync();
     const int mlm = s_mo[mw], mM = s_mo[mw + 1] - mlm, mlb = s_eo[mw];
-    int io0 = 0, io1 = 0;
-    if (is_mass) {
-        const uint32_t io = (uint32_t)(P0 + lane) + (uint32_t)(w0 + mw);   // inc_off: M_w + 1 per walker
-        io0 = b.inc_off[io]; io1 = b.inc_off[io + 1];
-    }
+    // inc_off (M_w + 1 entries per walker) and the action: the second (and last) round of vector loads
+    const uint32_t io = (uint32_t)lp + (uint32_t)(w0 + mw);
+    int io0 = b.inc_off[io], io1 = b.inc_off[io + 1];
     const int ua = lane - s_uo[uw];                                      // this lane's muscle in walker uw
     const bool acts = action != nullptr && is_mus && ua < action_cols;
     float act = 0.f;
-    if (acts) act = action[(size_t)s_row[uw] * action_stride + ua];
+    if (action && action_cols > 0)
+        act = action[(size_t)s_row[uw] * action_stride + min(max(ua, 0), action_cols - 1)];
+    // the reference values of the lanes past the tile's masses / muscles (the loads above read duplicates)
+    if (!is_mass) {
+        p3[0] = 0.f; p3[1] = 0.f; p3[2] = 0.f; v3[0] = 0.f; v3[1] = 0.f; v3[2] = 0.f;
+        mf = 0.f; pin = 0; io0 = 0; io1 = 0;
+    }
+    if (!is_mus) { mx = 0.f; mlo = 0.f; mhi = 0.f; mst = 0.f; }
+    if (!acts) act = 0.f;
     if (kp.prio) __builtin_amdgcn_s_setprio(0);
     STAMP(1);
 

@@ -106,3 +106,51 @@ def test_concat_specs_matches_creatures_to_spec():
         assert np.array_equal(joined[k], ref[k]), k
     h = pack(joined)
     assert h.N == 5 and h.ragged   # Box-v0 has 4 muscles, Balance-v0 2: a ragged batch
+
+
+def test_wave_edge_passes_matches_library():
+    """layout.wave_edge_passes restates walker_hip.hip wave_passes (wg_wave_edge_passes)."""
+    import ctypes as C
+    from walker_gym_amd import _lib
+    from walker_gym_amd.layout import wave_edge_passes
+    L = _lib.load()
+    for M in (0, 1, 2, 4, 13, 32, 64, 65):
+        for K in (0, 1, 5, 63, 64, 65, 128, 200, 300, 512, 513, 600):
+            assert wave_edge_passes(M, K) == L.wg_wave_edge_passes(C.c_int32(M), C.c_int32(K)), (M, K)
+
+
+def test_wave_tile_order_fills_tiles_and_planner_reproduces_them():
+    """Ragged batches whose walkers fit one wave are stored in best-fit-decreasing wave-tile order: every tile within
+    the wave caps, wg_plan_waves' greedy contiguous packing of that order yields exactly those tiles, and far fewer
+    of them than size-sorted neighbours (config 5's distribution)."""
+    import ctypes as C
+    from walker_gym_amd import _lib
+    from walker_gym_amd.layout import WAVE_LANES, size_order, wave_edge_passes
+    spec = ragged_walkers(3000, seed=5)
+    lay = pack(spec)
+    assert lay.row is not None and sorted(lay.row.tolist()) == list(range(3000))
+    assert np.array_equal(size_order(spec), lay.row)
+    L = _lib.load()
+
+    def plan(mo, eo, uo):
+        N = len(mo) - 1
+        out = np.zeros(N + 1, np.int32)
+        mo, eo, uo = (np.ascontiguousarray(x, np.int32) for x in (mo, eo, uo))
+        nb = L.wg_plan_waves(mo.ctypes.data_as(C.c_void_p), eo.ctypes.data_as(C.c_void_p),
+                             uo.ctypes.data_as(C.c_void_p), N, out.ctypes.data_as(C.c_void_p), N + 1)
+        assert nb > 0
+        return out[:nb + 1]
+    p = plan(lay.mass_off, lay.edge_off, lay.muscle_off)
+    Ms, Ks, As = np.diff(lay.mass_off), np.diff(lay.edge_off), np.diff(lay.muscle_off)
+    ne = wave_edge_passes(int(Ms.max()), int(Ks.max()))
+    for t in range(len(p) - 1):
+        a, b = p[t], p[t + 1]
+        assert Ms[a:b].sum() <= WAVE_LANES and Ks[a:b].sum() <= 64 * ne and As[a:b].sum() <= WAVE_LANES
+    # size-sorted neighbours (the previous order) for comparison
+    srt = np.lexsort((np.arange(3000), np.asarray(spec["n_muscles"]), np.diff(spec["edge_off"]),
+                      np.diff(spec["mass_off"])))
+    M0, K0, A0 = np.diff(spec["mass_off"])[srt], np.diff(spec["edge_off"])[srt], np.asarray(spec["n_muscles"])[srt]
+    p0 = plan(np.concatenate([[0], np.cumsum(M0)]), np.concatenate([[0], np.cumsum(K0)]),
+              np.concatenate([[0], np.cumsum(A0)]))
+    assert len(p) < 0.92 * len(p0), (len(p), len(p0))
+    assert Ms.sum() / (len(p) - 1) > 62.0

@@ -167,12 +167,19 @@ __device__ inline float np_dot3(float ax, float ay, float az, float bx, float by
 // numpy float32 pairwise summation (the add.reduce inner loop behind np.mean / np.sum) over a
 // strided LDS array: < 8 sequential; <= 128 eight interleaved partial sums; above that numpy
 // recurses on halves split at a multiple of 8.
-__device__ inline float pw_leaf(const float *a, int n, int st) {
-    if (n < 8) {
-        float r = 0.f;
-        for (int i = 0; i < n; i++) r += a[i * st];
-        return r;
+// r + a[0] + a[st] + ... (n terms) left to right, the reads issued four at a time ahead of their adds (one LDS
+// round trip per four terms instead of one per term; the same additions in the same order)
+__device__ inline float seq_sum_lds(float r, const float *a, int n, int st) {
+    int i = 0;
+    for (; i + 4 <= n; i += 4) {
+        const float x0 = a[i * st], x1 = a[(i + 1) * st], x2 = a[(i + 2) * st], x3 = a[(i + 3) * st];
+        r = (((r + x0) + x1) + x2) + x3;
     }
+    for (; i < n; i++) r += a[i * st];
+    return r;
+}
+__device__ inline float pw_leaf(const float *a, int n, int st) {
+    if (n < 8) return seq_sum_lds(0.f, a, n, st);
     float r0 = a[0], r1 = a[st], r2 = a[2 * st], r3 = a[3 * st];
     float r4 = a[4 * st], r5 = a[5 * st], r6 = a[6 * st], r7 = a[7 * st];
     int i = 8;
@@ -181,9 +188,8 @@ __device__ inline float pw_leaf(const float *a, int n, int st) {
         r0 += p[0]; r1 += p[st]; r2 += p[2 * st]; r3 += p[3 * st];
         r4 += p[4 * st]; r5 += p[5 * st]; r6 += p[6 * st]; r7 += p[7 * st];
     }
-    float res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
-    for (; i < n; i++) res += a[i * st];
-    return res;
+    const float res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+    return seq_sum_lds(res, a + i * st, n - i, st);
 }
 template <int D>
 __device__ inline float pw_tree(const float *a, int n, int st) {
@@ -1094,8 +1100,7 @@ __global__ __launch_bounds__(MAXT) void walker_step_kernel(
                                  : r == 4 ? s.nrm + lm : r == 5 ? s.ke + lm : s.pe + lm;
                 const int st = r <= 3 ? 3 : 1;
                 if (r < 3) {
-                    v = 0.f;
-                    for (int q = 0; q < M; q++) v += src[q * st];
+                    v = seq_sum_lds(0.f, src, M, st);
                 } else {
                     v = np_pairwise<PWD>(src, M, st);
                 }
@@ -1996,8 +2001,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
             const unsigned long long wm = (M == 64) ? ~0ull : (((1ull << M) - 1ull) << lm);
             v = __int_as_float((__popcll(hb & wm) << 1) | ((sb & wm) == wm ? 1 : 0));
         } else if (r < 3) {
-            v = 0.f;
-            for (int q = 0; q < M; q++) v += s_tp[3 * (lm + q) + r];
+            v = seq_sum_lds(0.f, s_tp + 3 * lm + r, M, 3);
         } else {
             const float *src = r == 3 ? s_tp + 3 * lm + 1 : r == 4 ? s_tn + lm : r == 5 ? s_tk + lm : s_te + lm;
             v = np_pairwise<0>(src, M, r == 3 ? 3 : 1);

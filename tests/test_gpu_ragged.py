@@ -1,6 +1,6 @@
 """Ragged batches on the GPU, through the C ABI:
 
-* the wave kernel (wg_batch.ragged = 2: walkers sorted by size, packed into wave tiles by wg_plan_waves) is
+* the wave kernel (wg_batch.ragged = 2: walkers stored in best-fit wave-tile order, tiles planned by wg_plan_waves) is
   bitwise equal to the workgroup kernel running the same plan (WG_LEAN=0), and both to the oracle with the
   outputs back in the caller's walker order;
 * pair forces (gym/engine.py:114-147 per walker) on the workgroup kernel: ragged batches and uniform walkers

@@ -394,7 +394,7 @@ class BatchedPhysicsEnv:
         return {"steps": self.batch.caller("steps"), "centroid_position": self.centroid, "total_energy": self.energy}
 
     # state accessors in the caller's order: live views into the batch, or gathered copies for a ragged batch
-    # (stored sorted by size; write through batch.to_stored / batch.stored_mass)
+    # (stored in wave-tile / size order; write through batch.to_stored / batch.stored_mass)
     @property
     def pos(self):
         return self.batch.caller("pos")

@@ -62,7 +62,7 @@ class DeviceBatch:
         self.radius = None   # allocated by enable_radius(): the step writes it, so only when bounce needs it
         # placeholders so that zero-size arrays still have a valid device pointer
         self._dummy = torch.zeros(16, dtype=torch.float32, device=dv)
-        # ragged batches are stored sorted by size (layout.pack): row = caller index of each stored walker
+        # ragged batches are stored in wave-tile / size order (layout.pack): row = caller index of each stored walker
         self.row = _to_dev(host.row, dv) if host.row is not None else None
         self._perm = {}
         if host.row is not None:
@@ -94,7 +94,7 @@ class DeviceBatch:
             self.plan_blocks = nb
         self.struct = self._make_struct()
 
-    # ---- the caller's order (ragged batches are stored sorted by size; uniform batches are not permuted)
+    # ---- the caller's order (ragged batches are stored in wave-tile / size order; uniform batches are not permuted)
     def caller(self, name: str) -> torch.Tensor:
         """A state tensor in the caller's walker / mass / muscle order: the tensor itself for an unpermuted batch
         (a live, writable view), a gathered copy for a sorted ragged batch."""

@@ -53,7 +53,7 @@ class HostLayout:
     pinned: Optional[np.ndarray] = None   # uint8 [P]: DingPoint masses (None = no pinned mass)
     charge: Optional[np.ndarray] = None   # float64 [P]: Point.e (None = Config.e for every point)
     radius: Optional[np.ndarray] = None   # float64 [P]: Point.r (None = m ** 0.3, gym/engine.py:45-46)
-    # ragged batches are stored sorted by size: row [N] = the caller's index of each stored walker, mass_perm /
+    # ragged batches are stored in wave-tile / size order (size_order): row [N] = the caller's index of each stored walker, mass_perm /
     # muscle_perm = the stored index of each caller mass / muscle (None = stored in the caller's order)
     row: Optional[np.ndarray] = None
     mass_perm: Optional[np.ndarray] = None
@@ -127,8 +127,8 @@ def incidence(ei: np.ndarray, ej: np.ndarray, mass_off: np.ndarray, edge_off: np
 
 def pack(spec: Dict[str, np.ndarray], mx: Optional[np.ndarray] = None, steps: Optional[np.ndarray] = None,
          sort: bool = True) -> HostLayout:
-    """Pack a flat CSR spec (see walker_gym_amd.synthetic) into the HBM layout.  A ragged batch is stored sorted
-    by walker size (``sort``; HostLayout.row / mass_perm / muscle_perm map it back to the caller's order)."""
+    """Pack a flat CSR spec (see walker_gym_amd.synthetic) into the HBM layout.  A ragged batch is stored in
+    size_order (``sort``; HostLayout.row / mass_perm / muscle_perm map it back to the caller's order)."""
     if mx is not None:
         spec = dict(spec, mx=mx)
     if steps is not None:

@@ -154,3 +154,32 @@ def test_wave_tile_order_fills_tiles_and_planner_reproduces_them():
               np.concatenate([[0], np.cumsum(A0)]))
     assert len(p) < 0.92 * len(p0), (len(p), len(p0))
     assert Ms.sum() / (len(p) - 1) > 62.0
+
+
+def test_wave_tile_order_caps_and_reproduction_edge_cases():
+    """Best-fit wave tiles under each cap in turn (the walker-count cap with 1-mass walkers, the spring cap with
+    spring-dense walkers, the muscle cap), and wg_plan_waves' greedy pass over the order reproduces them."""
+    import ctypes as C
+    from walker_gym_amd import _lib
+    from walker_gym_amd.layout import wave_edge_passes, wave_tile_order
+    L = _lib.load()
+    rng = np.random.default_rng(11)
+    cases = [(np.ones(100, np.int64), np.zeros(100, np.int64), np.zeros(100, np.int64)),             # 32 walkers/tile
+             (rng.integers(4, 9, 300), rng.integers(20, 64, 300), np.zeros(300, np.int64)),           # springs bind
+             (rng.integers(2, 12, 300), rng.integers(0, 10, 300), rng.integers(0, 40, 300)),          # muscles bind
+             (rng.integers(1, 65, 500), rng.integers(0, 65, 500), rng.integers(0, 13, 500))]
+    for Ms, Ks, As in cases:
+        ne = wave_edge_passes(int(Ms.max()), int(Ks.max()))
+        order = wave_tile_order(Ms, Ks, As, ne)
+        assert sorted(order.tolist()) == list(range(len(Ms)))
+        mo, eo, uo = (np.concatenate([[0], np.cumsum(x[order])]).astype(np.int32) for x in (Ms, Ks, As))
+        plan = np.zeros(len(Ms) + 1, np.int32)
+        nb = L.wg_plan_waves(mo.ctypes.data_as(C.c_void_p), eo.ctypes.data_as(C.c_void_p),
+                             uo.ctypes.data_as(C.c_void_p), len(Ms), plan.ctypes.data_as(C.c_void_p), len(Ms) + 1)
+        assert nb > 0
+        for t in range(nb):
+            a, b = plan[t], plan[t + 1]
+            assert mo[b] - mo[a] <= 64 and eo[b] - eo[a] <= 64 * ne and uo[b] - uo[a] <= 64 and b - a <= 32
+        # the lower bound on tiles from masses alone is met within a tile or two where masses bind
+        if Ks.max() == 0:
+            assert nb == -(-len(Ms) // 32)

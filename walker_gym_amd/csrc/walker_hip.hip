@@ -1964,7 +1964,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
     float px = 0.f, py = 0.f, pz = 0.f, vx = 0.f, vy = 0.f, vz = 0.f, ax = 0.f, ay = 0.f, az = 0.f;
     bool hit = false;
     if (is_mass) {
-        mass_accumulate<TermsAoS, false>(ts, reinterpret_cast<const uint16_t *>(s_inc) + 2 * mlb, mlb, io0, io1, mf, ax,
+        mass_accumulate<TermsAoS, true>(ts, reinterpret_cast<const uint16_t *>(s_inc) + 2 * mlb, mlb, io0, io1, mf, ax,
                                             ay, az, 0);
         mass_tail(kp, mf, (float)ym, p3, v3, px, py, pz, vx, vy, vz, ax, ay, az, hit, pin != 0);
         const uint32_t pl = (uint32_t)(P0 + lane);

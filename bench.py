@@ -225,21 +225,33 @@ def main():
     backend = os.environ.get("WG_DIST_BACKEND", "nccl")   # nccl = RCCL; gloo only to rehearse ranks on one GPU
     if backend != "nccl":
         local = local % max(1, torch.cuda.device_count())
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
+    # inside a torch.distributed world (WORLD_SIZE set by torch.distributed.run), world 1 included: the process
+    # group and the rollout-end gather run at every N, so `torchrun --nproc-per-node 1 bench.py` executes exactly
+    # the code of the 8-GPU run (RCCL init, barriers, max-over-ranks wall time, all_gather_into_tensor)
+    in_world = "WORLD_SIZE" in os.environ
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+
+    def init_group():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+
+    # the process group comes up after the env's walker-range streams exist and have run the warm-up: RCCL's own
+    # streams then cannot take the hardware queue a side stream would otherwise get (BatchedPhysicsEnv.__init__);
+    # WG_DIST_INIT_FIRST=1 (diagnostic) restores the other order
+    dist_first = os.environ.get("WG_DIST_INIT_FIRST", "0") == "1"
+    if in_world and dist_first:
+        init_group()
 
     N = args.walkers
     spec, params = make_spec(args.workload, N, seed=1000 + rank, chain_points=args.chain_points)
     env = BatchedPhysicsEnv(spec, device=dev, **params)
     A = max(1, env.batch.A)
     lanes = env._lanes(args.lanes)
+    env.reserve_streams(lanes)
     gen = torch.Generator(device=dev)
     gen.manual_seed(7 + rank)
     acts_w = (torch.rand((max(args.warmup, 1), N, A), generator=gen, device=dev) * 2 - 1).contiguous()
@@ -252,7 +264,9 @@ def main():
     if graph is not None:
         graph.replay()                         # warm the graph path too
     torch.cuda.synchronize()
-    if world > 1:
+    if in_world and not dist_first:
+        init_group()
+    if in_world:
         dist.barrier()
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -263,17 +277,19 @@ def main():
     else:
         env.run(acts, args.steps, lanes=lanes)
     ev1.record(stream)
-    if world > 1 and not args.no_gather:
-        gather_rollout(env.obs)                # rollout-end observation gather (RCCL all_gather_into_tensor)
+    gathered = None
+    if in_world and not args.no_gather:
+        # rollout-end observation gather (RCCL all_gather_into_tensor), shard sizes from shard_bounds
+        gathered = gather_rollout(env.obs, n_total=world * N)
     torch.cuda.synchronize()
-    if world > 1:
+    if in_world:
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     step_ms = ev0.elapsed_time(ev1) / args.steps
 
     wall_t = torch.tensor([wall], dtype=torch.float64, device=dev)
-    if world > 1:
+    if in_world:
         dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
     wall_max = float(wall_t.item())
 
@@ -323,7 +339,10 @@ def main():
                                    f"({lanes} range{'s' if lanes > 1 else ''} on {lanes} stream{'s' if lanes > 1 else ''})"
                                    + (", replayed as one HIP graph" if graph is not None else ""),
                        "walkers_per_gpu": N, "total_walkers": world * N, "M": M, "K": K, "A": env.batch.A,
-                       "obs_dim": D, "parallelism": f"dp{world}", "rollout_gather": world > 1 and not args.no_gather,
+                       "obs_dim": D, "parallelism": f"dp{world}", "rollout_gather": gathered is not None,
+                       "dist_backend": (dist.get_backend() if in_world else None),
+                       **({"dist_init": "before the env" if dist_first else "after the env's streams and warm-up"}
+                          if in_world else {}),
                        "lanes": lanes, "launch": geo, "ragged_kind": env.batch.ragged_kind,
                        **({"chain_points": args.chain_points, "pair_mode": 1} if args.workload == "chain" else {})},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -364,7 +383,7 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.workload, params, args.chain_points, args.cpu_seconds)
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if in_world:
         dist.destroy_process_group()
 
 

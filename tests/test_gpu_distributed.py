@@ -61,3 +61,25 @@ def test_two_ranks_bitwise_equal_one_rank_and_oracle(tmp_path, n_total):
         np.testing.assert_allclose(one["reward"][t], ref["reward"], atol=1e-4, rtol=1e-5)
         assert np.array_equal(one["done"][t], ref["done"])
     np.testing.assert_allclose(one["pos"].reshape(-1, 3), orc.pos, atol=1e-4, rtol=1e-5)
+
+
+def test_rccl_one_rank_gather_rollout_on_device(tmp_path):
+    """The RCCL transport of BASELINE config 4 on hardware: a fresh torch.distributed.run child with one rank on
+    cuda:0 over nccl (= RCCL) runs gather_rollout on device tensors (tests/nccl_rank.py) — n_total given and
+    omitted, an odd row count, f32 and u8 rollouts — and every gather must return its input bitwise."""
+    if not gpu_available():
+        pytest.skip("no ROCm GPU")
+    import json
+    out = str(tmp_path / "nccl.json")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(HERE, "nccl_rank.py"), out]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240,
+                       env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.load(open(out))
+    assert res["backend"] == "nccl" and res["world"] == 1
+    assert res["wrong_n_total_refused"]
+    assert len(res["checks"]) == 6
+    for name, c in res["checks"].items():
+        assert c["device"].startswith("cuda"), name
+        assert c["shape_ok"] and c["dtype_ok"] and c["bitwise"], (name, c)

@@ -136,6 +136,12 @@ class BatchedPhysicsEnv:
             self._gen.manual_seed(int(seed))
         self._generation = 0
         self._alloc_outputs()
+        # the side streams of the default walker ranges, created now: a stream's hardware queue is bound when it is
+        # created, and a process has few of them (GPU_MAX_HW_QUEUES = 4).  Created after an RCCL communicator
+        # (whose streams take queues of their own) a side stream can share the calling stream's queue, which
+        # serialises the ranges: 52.8 against 37.5 us per canonical step (profiles/r03a_bench_nccl1.json).
+        self._side = []
+        self.reserve_streams(self._lanes(None))
 
     @classmethod
     def from_topologies(cls, topologies, n_envs: int, device=None, **params) -> "BatchedPhysicsEnv":
@@ -303,6 +309,13 @@ class BatchedPhysicsEnv:
             return max(1, min(lanes, self.batch.plan_blocks // 64))
         return 1 if self.N < 64 * lanes else lanes
 
+    def reserve_streams(self, lanes: int) -> None:
+        """Side streams for `lanes` walker ranges (lanes - 1 of them; existing ones are kept, so their hardware
+        queues stay bound).  Call before creating other streams (an RCCL process group) to keep the ranges on
+        queues of their own."""
+        while len(self._side) < lanes - 1:
+            self._side.append(torch.cuda.Stream(device=self.device))
+
     def _run_lanes(self, actions, n_steps: int, outputs, lanes: int, entry: str = "wg_step"):
         """n_steps with the walkers split into `lanes` contiguous ranges, each stepped by its own stream: the
         ranges are independent, so one range's step t + 1 fills the GPU while another's step t drains (the
@@ -311,8 +324,7 @@ class BatchedPhysicsEnv:
         the WgOutputs of walkers [w0, w1)."""
         T, n, cols = actions.shape
         cur = torch.cuda.current_stream(self.device)
-        if len(getattr(self, "_side", [])) != lanes - 1:
-            self._side = [torch.cuda.Stream(device=self.device) for _ in range(lanes - 1)]
+        self.reserve_streams(lanes)
         start = torch.cuda.Event()
         start.record(cur)
         L = _lib.load()

@@ -36,6 +36,18 @@ sys.path.insert(0, ROOT)
 
 METRIC = "env-steps/sec (whole node) at 65 536 walkers; 1/2/4/8 MI355X scaling"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+# vector (non-matrix) VALU peaks: FP32 157.3 TFLOP/s is MI355X_MICROARCH.md's (v_pk_fma_f32); the guide lists no FP64
+# figure, so FP64 is AMD's MI355X datasheet vector FP64, 78.6 TFLOP/s (= the FP32 rate without packing: one v_fma_f64
+# per lane per 2 cycles); scripts/valu_peak.hip measures both on the box (profiles/r03_valu_peak.json)
+FP64_PEAK_TFS = 78.6
+FP32_PEAK_TFS = 157.3
+# algorithmic FLOP per unordered pair of the reference's pair loops:
+#   chain (gym/engine.py:128-137 + anti_forced :69-76): 3 norms x 2 float64 adds, r**2, two products and the
+#     quotient of f, and per end 3 products, 3 quotients by r, 3 by m, 3 adds: 34 FP64
+#   perfdemo (gym/optimized_engine.py:177-193, gravity_vec): float32 norm (3 products, sqrt) and powf, the quotient
+#     of f, 3 products and 3 quotients of the force, and per end 3 quotients by m and 3 adds: 24 FP32
+#     (+ the norm's 2 float64 adds and the numerator's 2 float64 products)
+PAIR_FLOP = {"chain": (34, "fp64-valu", FP64_PEAK_TFS), "perfdemo": (24, "fp32-valu", FP32_PEAK_TFS)}
 
 
 def parse(argv=None):
@@ -44,7 +56,8 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=1000)   # time 1,000 steps after 50
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--walkers", type=int, default=65536, help="walkers per GPU")
-    ap.add_argument("--workload", default="canonical", choices=["canonical", "balance", "ragged", "chain", "lattice25"])
+    ap.add_argument("--workload", default="canonical",
+                    choices=["canonical", "balance", "ragged", "chain", "perfdemo", "lattice25"])
     ap.add_argument("--chain-points", type=int, default=100, help="masses per chain walker (--workload chain)")
     ap.add_argument("--lanes", type=int, default=None, help="walker ranges on separate streams (default: auto)")
     ap.add_argument("--resident", action="store_true", help="also time the K steps as ONE wg_rollout launch (state in "
@@ -109,8 +122,10 @@ def make_spec(workload: str, n: int, seed: int, chain_points: int = 100):
         return canonical_walkers(n, seed=seed), dict(in3d=1)
     if workload == "balance":
         return balance_spec(n), dict(in3d=0)
-    if workload == "chain":
+    if workload == "chain":      # engine.py Point.gravity (float64 anti_forced path) after the springs
         return chain_walkers(n, chain_points, seed=seed), dict(in3d=1, g=0.0, ground=-1.0e6, pair_mode=1)
+    if workload == "perfdemo":   # the performance_demo loop as written: G2 Point.gravity = gravity_vec (float32)
+        return chain_walkers(n, chain_points, seed=seed), dict(in3d=1, g=0.0, ground=-1.0e6, pair_mode=8)
     if workload == "lattice25":
         return canonical_walkers(n, seed=seed, M=25, K=60, A=10), dict(in3d=1)
     return ragged_walkers(n, seed=seed, mmin=4, mmax=32), dict(in3d=1)
@@ -122,8 +137,13 @@ DATA = {"canonical": "synthetic (seeded; SURVEY §8(d) canonical walker M=16, K=
                    "step)",
         "ragged": "synthetic (seeded mixed topologies, M ~ U{4..32}, K ~ U{M..2M}, A = K // 5; U(-1,1) actions, "
                   "distinct per step)",
-        "chain": "synthetic (performance_demo chain: U(-100,100) positions, U(-10,10) velocities, Skeleton(k=50) "
-                 "links, per-walker Point.gravity; no muscles)",
+        "chain": "synthetic (performance_demo's chain topology: U(-100,100) positions, U(-10,10) velocities, "
+                 "Skeleton(k=50) links, then gym/engine.py's Point.gravity per walker after the springs (the float64 "
+                 "anti_forced path); no muscles)",
+        "perfdemo": "synthetic (the performance_demo loop as written, gym/performance_demo.py:52-58, per walker: "
+                    "creature.run(); Point.gravity() = optimized_engine gravity_vec (zeroes a, float32 pairs, "
+                    "powf distance ** 2); Point.run1(0.01); chain topology, U(-100,100) positions, U(-10,10) "
+                    "velocities)",
         "lattice25": "synthetic (seeded uniform 5x5-lattice walkers, M=25 (not a divisor of 64), K=60, A=10; U(-1,1) "
                      "actions, distinct per step)"}
 
@@ -149,7 +169,8 @@ def cpu_baseline(workload, params, chain_points, budget_s: float) -> dict:
     from oracle.oracle import Oracle
     from oracle.refstyle import host_cores, throughput
     cores = host_cores()
-    rs_n = 8 if workload == "chain" else 32
+    pairs = workload in ("chain", "perfdemo")
+    rs_n = 8 if pairs else 32
     spec = make_spec(workload, rs_n, 99, chain_points)[0]
     A = max(1, int(np.max(spec["n_muscles"])))
     acts = np.random.default_rng(123).uniform(-1, 1, (8, rs_n, A)).astype(np.float32)
@@ -157,7 +178,7 @@ def cpu_baseline(workload, params, chain_points, budget_s: float) -> dict:
     rs1 = throughput(spec, params, acts, share)
     rs1p = throughput(spec, params, acts, share, observe=False)
     rsn = throughput(spec, params, acts, share, procs=cores)
-    n = 512 if workload == "chain" else 4096
+    n = 512 if pairs else 4096
     spec = make_spec(workload, n, 99, chain_points)[0]
     acts = np.random.default_rng(123).uniform(-1, 1, (8, n, A)).astype(np.float32)
     res = {}
@@ -302,6 +323,21 @@ def main():
             env.run(acts[:n1], n1, lanes=1)
             single_ms = timed(env, acts[:n1], n1, 1, stream)
         direct_ms = timed(env, acts, args.steps, lanes, stream) if graph is not None else None
+        # closed loop: one BatchedPhysicsEnv.step per env step, as a policy loop calls it (the walker ranges join
+        # at the end of every step, and every step returns obs/reward/done/info); the headline `value` instead
+        # issues the K steps back to back (open loop: actions known up front, ranges drift out of phase)
+        closed_ms = None
+        if not args.no_control:
+            n_cl = max(20, min(args.steps, 200))
+            for s_ in range(5):
+                env.step(acts[s_])
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for s_ in range(n_cl):
+                env.step(acts[s_])
+            e1.record(stream)
+            torch.cuda.synchronize()
+            closed_ms = e0.elapsed_time(e1) / n_cl
         resident_ms = None
         if args.resident:
             env.run(acts[:n1], n1, lanes=1, resident=True)
@@ -344,7 +380,8 @@ def main():
                        **({"dist_init": "before the env" if dist_first else "after the env's streams and warm-up"}
                           if in_world else {}),
                        "lanes": lanes, "launch": geo, "ragged_kind": env.batch.ragged_kind,
-                       **({"chain_points": args.chain_points, "pair_mode": 1} if args.workload == "chain" else {})},
+                       **({"chain_points": args.chain_points, "pair_mode": params["pair_mode"]}
+                          if args.workload in PAIR_FLOP else {})},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": (tr["hbm_bytes_per_launch"] if tr else None),
@@ -368,6 +405,13 @@ def main():
         if graph is not None:
             line["graph"] = {"replay_ms_per_step": round(step_ms, 5), "direct_ms_per_step": round(direct_ms, 5),
                              "launch_overhead_share": round(max(0.0, 1 - step_ms / direct_ms), 4)}
+        if closed_ms is not None:
+            line["closed_loop"] = {
+                "ms_per_step": round(closed_ms, 5), "env_steps_per_s": round(N * 1e3 / closed_ms, 1),
+                "lanes": env._lanes(None),
+                "note": "BatchedPhysicsEnv.step() once per env step (HIP events on the calling stream over 20-200 "
+                        "steps): the walker ranges join every step and each step returns obs / reward / done / info "
+                        "— what a policy loop gets; `value` is the open-loop rate (K steps issued back to back)"}
         if resident_ms is not None:
             line["resident_rollout"] = {
                 "ms_per_step": round(resident_ms, 5), "env_steps_per_s": round(N * 1e3 / resident_ms, 1),
@@ -377,8 +421,22 @@ def main():
                         "headline, which is one launch per env step (SURVEY 8(d))"}
         if tr:
             line["roofline"]["traffic_source"] = tr.get("source")
-        if args.workload == "chain":
+        if args.workload in PAIR_FLOP:
+            # O(M^2) per walker: the partner loops, not HBM, bound these launches; the roofline is the VALU's
+            flop_pair, bound, peak = PAIR_FLOP[args.workload]
             pairs = N * args.chain_points * (args.chain_points - 1) / 2
+            tfs = pairs * flop_pair / (head_ms * 1e-3) / 1e12
+            hbm = dict(line["roofline"])
+            line["roofline"] = {"bound": bound, "achieved": round(tfs, 3), "peak": peak, "unit": "TFLOP/s",
+                                "frac": round(tfs / peak, 4), "traffic": hbm.get("traffic"),
+                                "flop_per_pair": flop_pair, "pairs_per_launch": int(pairs),
+                                "flop_per_launch": int(pairs * flop_pair), "kernel_ms_per_launch": round(head_ms, 5),
+                                "note": ("achieved = the reference pair loop's algorithmic FLOP per unordered pair x "
+                                         "the pairs of one launch (N * M(M-1)/2) / the per-launch time of ONE "
+                                         "full-batch launch (HIP events); peak = the vector "
+                                         + ("FP64" if bound == "fp64-valu" else "FP32") + " rate (bench.py "
+                                         "FP64_PEAK_TFS / FP32_PEAK_TFS, measured by scripts/valu_peak.hip)"),
+                                "hbm": {k: hbm[k] for k in ("achieved", "peak", "unit", "frac", "bytes_per_walker_step")}}
             line["pairs_per_s"] = round(pairs / (head_ms * 1e-3), 1)
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.workload, params, args.chain_points, args.cpu_seconds)

@@ -151,6 +151,14 @@ class Oracle:
             _p(self.maxl, _f32p), _p(self.stride, _f32p), _p(self.steps, _i32p), _p(self.contact, _u8p),
             _p(self.pinned, _u8p), _p(self.charge, _f64p), _p(self.radius, _f64p))
 
+    def set_params(self, **kw):
+        """Change env parameters between steps (the state stays), as BatchedPhysicsEnv.set_params."""
+        for k, v in kw.items():
+            if k not in self.params:
+                raise KeyError(k)
+            self.params[k] = v
+        self._mk_structs()
+
     def _outs(self):
         o = dict(obs=np.zeros((self.N, self.obs_stride), np.float32), reward=np.zeros(self.N, np.float32),
                  done=np.zeros(self.N, np.uint8), centroid=np.zeros((self.N, 3), np.float32),

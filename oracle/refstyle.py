@@ -114,6 +114,20 @@ class RWalker:
                     f = -P["pair_g"] * pts[i].m * pts[j].m / (r ** 2)
                     pts[j].anti_forced(f, pts[i])
                     pts[i].anti_forced(f, pts[j])
+        if P["pair_mode"] & 8 and len(self.phys) >= 2:           # G2 Point.gravity = gravity_vec,
+            pts = self.phys                                       # gym/optimized_engine.py:167-193
+            for p in pts:
+                p.zero()
+            for i in range(len(pts)):
+                for j in range(i + 1, len(pts)):
+                    p1, p2 = pts[i], pts[j]
+                    direction = p2.pos - p1.pos
+                    distance = np.linalg.norm(direction)
+                    distance = max(distance, CONFIG_R)
+                    f = -P["pair_g"] * p1.m * p2.m / (distance ** 2)
+                    force = f * direction / distance
+                    p1.forced(force)
+                    p2.forced(-force)
         g, dampk, ground = P["g"], P["dampk"], P["ground"]
         for p in self.phys:                                       # gym/optimized_env.py:146-172
             p.forced(np.array([0, -g, 0], dtype=f32))

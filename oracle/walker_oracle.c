@@ -284,6 +284,46 @@ static void walker_step(const orc_batch *b, const orc_params *p, int w, const fl
                 for (int c = 0; c < 3; c++) acc[3 * i + c] = add_f64(acc[3 * i + c], (double)(nf * (ps[c] - pi[c])) / dist, b->m[i]);
             }
     }
+    /*     G2 Point.gravity = gravity_vec (gym/optimized_engine.py:167-197; the performance_demo loop's N-body,
+     *     gym/performance_demo.py:52-58): with >= 2 points every a is zeroed first (:174-175, discarding the
+     *     springs above), then for each pair i < j: direction = p_j - p_i; distance = norm(direction), a numpy
+     *     float32 (no .astype(float), :185-186); max(distance, Config.r); f = -Config.g * m_i * m_j / distance ** 2
+     *     (:189: the Python-float numerator weakly cast to float32, distance ** 2 = libm powf); force = f *
+     *     direction / distance (:192, float32); p_i.forced(force), p_j.forced(-force) (:193-194, float32 a += f/m).
+     *     A clamped distance is the Python float Config.r: f and the division by it then take its float32 casts. */
+    if ((p->pair_mode & 8) && m1 - m0 >= 2) {
+        for (int q = m0; q < m1; q++) acc[3 * q] = acc[3 * q + 1] = acc[3 * q + 2] = 0.f;
+        for (int i = m0; i < m1; i++)
+            for (int j = i + 1; j < m1; j++) {
+                const float *pi = pos + 3 * i, *pj = pos + 3 * j;
+                const float d[3] = {pj[0] - pi[0], pj[1] - pi[1], pj[2] - pi[2]};
+                const float dist = np_norm3(d[0], d[1], d[2]);
+                const double num = (-p->pair_g * (double)b->m[i]) * (double)b->m[j];
+                float f, dv;
+                if (CONFIG_R > (double)dist) { f = (float)(num / (CONFIG_R * CONFIG_R)); dv = (float)CONFIG_R; }
+                else { f = (float)num / powf(dist, 2.0f); dv = dist; }
+                for (int c = 0; c < 3; c++) {
+                    const float force = (f * d[c]) / dv;
+                    acc[3 * i + c] = add_f32(acc[3 * i + c], force, b->m[i]);
+                    acc[3 * j + c] = add_f32(acc[3 * j + c], -force, b->m[j]);
+                }
+            }
+    }
+    /*     Point.electrostatic (gym/engine.py:150-158) of every point, in registry order: for every other point i,
+     *     r = max(norm(p_s - p_i) as float64, Config.r); f = -Config.k * e_s * e_i / r**2 (self's charge first);
+     *     s.anti_forced(f, i) (:69-76): only s receives (-f) * (p_i - p_s) / r in float64, divided by m. */
+    if (p->pair_mode & 16) {
+        for (int s = m0; s < m1; s++)
+            for (int i = m0; i < m1; i++) {
+                if (i == s) continue;
+                const float *ps = pos + 3 * s, *pi = pos + 3 * i;
+                double r = (double)np_norm3(ps[0] - pi[0], ps[1] - pi[1], ps[2] - pi[2]);
+                if (CONFIG_R > r) r = CONFIG_R;
+                const double es = b->charge ? b->charge[s] : p->pair_e, ei = b->charge ? b->charge[i] : p->pair_e;
+                const double f = ((-p->pair_k) * es) * ei / (r * r);
+                for (int c = 0; c < 3; c++) acc[3 * s + c] = add_f64(acc[3 * s + c], (-f) * (double)(pi[c] - ps[c]) / r, b->m[s]);
+            }
+    }
 
     /* 4. env forces per mass (gym/env.py:31-41, gym/optimized_env.py:146-172), each one Point.forced
      *    with a float32 force: gravity, linear damp, then (in contact) ground spring, ground damp,

@@ -20,7 +20,7 @@ objects, with SURVEY §8(c)'s mechanical fixes applied by overriding only the me
   the G1 friction force ``[v_x*deep*friction, 0, v_z*deep*friction]`` (:41).  Creatures: the G1 builders of
   gym/walker.py (make_golden.load_g1_walker).
 
-Scenarios (tests/golden/api/*.npz; the chain fixtures are engine-level and go to tests/golden/):
+Scenarios (tests/golden/api/*.npz):
   api_balance_2d       np.random.seed(123); PhysicsEnv(balance); seed(7); reset(); 60 steps of U(-1,1) actions
   api_box_3d_maxsteps  the same with Box-v0 in 3D, max_steps = 40, 45 steps: done from step 40 on
   api_settle           Balance-v0, dampk = 5, rand_sigma = 0, zero actions, 230 steps: every |v| < 0.1 after
@@ -29,9 +29,9 @@ Scenarios (tests/golden/api/*.npz; the chain fixtures are engine-level and go to
                        steps >= max_steps on the last step)
   g1_env               random.seed(5); G1 Environment([leg2, box, balance], in3d=True, randsigma=0.5, dampk=0.1);
                        50 step(t) calls with t cycling 0.01 / 0.005 / 0.02
-  chain_gravity        performance_demo's chain (gym/performance_demo.py:18-58) for N in
-                       {10, 50, 100, 200}: one walker each, Skeleton(k=50) links, the reference's Point.gravity over
-                       the walker's points after its springs, no env gravity (g = 0) and no ground; 40 steps
+Every output goes to --out (default tests/golden/api/); each scenario draws its actions from its own generator,
+seeded by its name, so scenarios never shift one another.  (The performance_demo chain fixtures are engine-level:
+make_golden.py.)
 """
 from __future__ import annotations
 
@@ -109,24 +109,25 @@ def record_env(env, actions, T):
             "out_acc": np.array(out["acc"], f32)}
 
 
-def main():
+def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
     ap.add_argument("--out", default=os.path.join(HERE, "api"))
-    args = ap.parse_args()
+    ap.add_argument("--only", nargs="*", default=None, help="run only these scenarios")
+    args = ap.parse_args(argv)
+    want = (lambda name: args.only is None or name in args.only)
     E, OW, OE = MG.load_reference(args.ref)
     os.makedirs(args.out, exist_ok=True)
     FixedEnv = fixed_physics_env(E, OW, OE)
-    rng = np.random.default_rng(20261016)
     written = []
 
     def fresh():
         E.Point.points = []
         E.Point.r_points = {}
 
-    def save(name, blob, out=None):
+    def save(name, blob):
         blob["numpy_version"] = np.array(np.__version__)
-        path = os.path.join(out or args.out, name + ".npz")
+        path = os.path.join(args.out, name + ".npz")
         np.savez_compressed(path, **blob)
         written.append((name, os.path.getsize(path)))
 
@@ -137,6 +138,8 @@ def main():
             ("api_settle", "balance", dict(in3d=False, dampk=5, rand_sigma=0.0), None, 230, "zero"),
             ("api_rollout_1000", "balance", dict(in3d=True), None, 1000, "zero")]
     for name, creature, kw, max_steps, T, acts_kind in scen:
+        if not want(name):
+            continue
         fresh()
         cr = {"balance": OW.create_balance_creature, "box": OW.create_box_creature}[creature]()
         np.random.seed(123)
@@ -146,7 +149,8 @@ def main():
         env.seed(7)
         obs0 = env.reset()                       # the second noise draw, after seed(7)
         A = len(cr.muscles)
-        actions = (rng.uniform(-1, 1, (T, A)).astype(f32) if acts_kind == "uniform" else np.zeros((T, A), f32))
+        actions = (MG.scenario_rng(name).uniform(-1, 1, (T, A)).astype(f32) if acts_kind == "uniform"
+                   else np.zeros((T, A), f32))
         rec = record_env(env, actions, T)
         blob = dict(env_id=np.array({"balance": "Balance-v0", "box": "Box-v0"}[creature]),
                     kwargs_in3d=np.array(int(kw.get("in3d", False))), kwargs_dampk=np.array(float(kw.get("dampk", 0))),
@@ -160,6 +164,13 @@ def main():
         print(name, "done steps:", np.nonzero(rec["out_done"])[0][:3] + 1)
 
     # ---- G1 Environment (gym/env.py) with G1 creatures
+    if want("g1_env"):
+        g1_env(args, E, OW, fresh, save)
+    for name, size in written:
+        print(f"{name:22s} {size:9d} B")
+
+
+def g1_env(args, E, OW, fresh, save):
     fresh()
     import gym.env as GE
     G1 = MG.load_g1_walker(args.ref, E)
@@ -189,26 +200,6 @@ def main():
     save("g1_env", dict(g1_names=np.array(names), random_seed=np.array(5), in3d=np.array(1), dampk=np.array(0.1),
                         randsigma=np.array(0.5), ts=np.array(ts), out_vel0=vel0, out_pos=np.array(pos, f32),
                         out_vel=np.array(vel, f32), out_acc=np.array(acc, f32)))
-
-    # ---- performance_demo chain with per-walker Point.gravity
-    from walker_gym_amd.synthetic import chain_walkers
-    for n_pts in (10, 50, 100, 200):
-        fresh()
-        spec = MG.Spec(**chain_walkers(1, n_pts, seed=n_pts))
-        crs = MG.creatures_from_spec(E, OW, spec)
-        run = MG.RefRun(E, OW, OE, crs, dict(in3d=1, g=0.0, ground=-1.0e6, pair_mode=1, pair_g=9.8))
-        outs = MG.record(run, None, 40, None)
-        blob = {}
-        blob.update(spec.arrays())
-        blob.update(MG.params_array(run.p))
-        blob["actions"] = np.zeros((40, 1, 0), f32)
-        blob["action_mode"] = np.array(0, np.int32)
-        blob["noise"] = np.zeros((0, 3), f32)
-        blob.update(outs)
-        save(f"chain_gravity_{n_pts}", blob, out=HERE)   # engine-level fixture: tests/golden/ with the others
-
-    for name, size in written:
-        print(f"{name:22s} {size:9d} B")
 
 
 if __name__ == "__main__":

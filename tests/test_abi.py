@@ -103,7 +103,7 @@ def test_errors_without_gpu(lib):
     b.row = None
     # unknown pair bits, and bounce without the radius array, are refused before any launch
     b.ragged = 0
-    for pm in (8, 4):
+    for pm in (32, 64 | 1, 4):
         p = _lib.WgParams(pair_mode=pm, bounce_k=100.0)
         assert lib.wg_step(C.byref(b), C.byref(p), None, 0, 0, 0, None, 1, None, 0, None) == _lib.WG_EINVAL
         assert b"pair_mode" in lib.wg_last_error()

@@ -6,7 +6,7 @@
   gym/optimized_env.py's PhysicsEnv with the SURVEY §8(c) fixes;
 * walker_gym_amd.env.Environment (G1): random.seed -> construction noise -> step(t) x 50 with varying t gives the
   states of gym/env.py's Environment, G1 friction included.
-Tolerance: bit-exact everywhere except the energy (numpy's float32 ** 2 is libm powf, the kernel x*x: rtol 1e-6).
+Tolerance: bit-exact everywhere (the energy's float32 ** 2 is libm powf, restated in walker_gym_amd/csrc/powf2.h).
 """
 import glob
 import os
@@ -50,7 +50,7 @@ def test_physicsenv_facade_matches_reference(path):
         assert isinstance(done, bool) and done == bool(z["out_done"][t]), t
         assert info["steps"] == z["out_steps"][t]
         assert isinstance(info["total_energy"], np.float32)
-        np.testing.assert_allclose(info["total_energy"], z["out_energy"][t], rtol=1e-6)
+        assert info["total_energy"] == z["out_energy"][t], t
         if (t + 1) % every == 0:
             s = (t + 1) // every - 1
             np.testing.assert_array_equal(obs, z["out_obs"][s])

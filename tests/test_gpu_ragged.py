@@ -81,8 +81,9 @@ def test_wave_kernel_vs_oracle_caller_order():
     assert np.array_equal(env.muscle_x.cpu().numpy(), orc.mx)
 
 
+@pytest.mark.parametrize("pair_mode", [7, 31])
 @pytest.mark.parametrize("case", ["ragged", "uniform_M13", "uniform_M100", "uniform_M100_wide"])
-def test_pair_forces_workgroup_kernel_vs_oracle(case):
+def test_pair_forces_workgroup_kernel_vs_oracle(case, pair_mode):
     import torch
     from oracle.oracle import Oracle
     from walker_gym_amd.batched_env import BatchedPhysicsEnv
@@ -102,8 +103,10 @@ def test_pair_forces_workgroup_kernel_vs_oracle(case):
     spec["radius"] = rng.uniform(0.5, 2.0, P)
     N = len(spec["mass_off"]) - 1
     A = max(1, int(np.max(spec["n_muscles"])))
-    params = dict(in3d=1, pair_mode=7, pair_g=500.0, pair_k=2.0e3, bounce_k=400.0)
+    params = dict(in3d=1, pair_mode=pair_mode, pair_g=500.0, pair_k=2.0e3, bounce_k=400.0)
     env = BatchedPhysicsEnv(spec, device="cuda:0", **params)
+    # pair forces run on the workgroup kernel, on a plan of its own (not the wave tiles)
+    assert env.batch.ragged_kind == (1 if case == "ragged" else 0), env.batch.ragged_kind
     if case == "uniform_M100_wide":
         info = env.launch_geometry()
         assert info["threads"] == 512 and info["walkers_per_block"] == 5, info
@@ -201,3 +204,70 @@ def test_rollout_into_dirty_buffer_zero_pads():
     lens = env.obs_len
     for w in range(N):
         assert (clean[:, w, lens[w]:] == 0).all()
+
+
+def test_plan_follows_params():
+    """A uniform batch whose M does not divide 64 (M = 25) runs wave tiles for engine springs without pair forces,
+    uniform workgroup tiles with pair forces; set_params re-plans both ways and every step stays bit-exact."""
+    import torch
+    from oracle.oracle import Oracle
+    from walker_gym_amd.batched_env import BatchedPhysicsEnv
+    from walker_gym_amd.synthetic import canonical_walkers
+    N = 700
+    spec = canonical_walkers(N, seed=61, M=25, K=60, A=10)
+    acts = np.random.default_rng(61).uniform(-1, 1, (9, N, 10)).astype(np.float32)
+    env = BatchedPhysicsEnv(spec, device="cuda:0", in3d=1)
+    orc = Oracle(spec, dict(in3d=1))
+    kinds = []
+    for t, pm in enumerate([0, 0, 0, 24, 24, 24, 0, 0, 0]):
+        if pm != env.params.pair_mode:
+            env.set_params(pair_mode=pm, pair_g=300.0)
+            orc.set_params(pair_mode=pm, pair_g=300.0)
+        kinds.append(env.batch.ragged_kind)
+        obs, rew, done, info = env.step(acts[t])
+        ref = orc.step(acts[t])
+        torch.cuda.synchronize()
+        assert np.array_equal(obs.cpu().numpy(), ref["obs"], equal_nan=True), t
+    assert kinds == [2, 2, 2, 0, 0, 0, 2, 2, 2]
+    assert np.array_equal(env.pos.cpu().numpy(), orc.pos, equal_nan=True)
+
+
+def test_state_dict_independent_of_storage_order():
+    """a ragged batch's storage order depends on WG_TILE_ORDER (read when the batch is packed); a state
+    dict saved under one order loads into a batch stored in another and both continue bit-identically."""
+    import torch
+    from walker_gym_amd.batched_env import BatchedPhysicsEnv
+    from walker_gym_amd.synthetic import ragged_walkers
+    N = 900
+    spec = ragged_walkers(N, seed=71, mmin=3, mmax=30)
+    A = int(np.max(spec["n_muscles"]))
+    acts = np.random.default_rng(71).uniform(-1, 1, (10, N, A)).astype(np.float32)
+    os.environ["WG_TILE_ORDER"] = "sorted"
+    try:
+        a = BatchedPhysicsEnv(spec, device="cuda:0", in3d=1)
+    finally:
+        del os.environ["WG_TILE_ORDER"]
+    b = BatchedPhysicsEnv(spec, device="cuda:0", in3d=1)
+    assert not np.array_equal(a.batch.host.row, b.batch.host.row)
+    a.rollout(acts[:5])
+    b.batch.load_state_dict(a.batch.state_dict())
+    oa, ra, _ = a.rollout(acts[5:])
+    ob, rb, _ = b.rollout(acts[5:])
+    torch.cuda.synchronize()
+    assert torch.equal(oa, ob) and torch.equal(ra, rb)
+    for k in ("pos", "vel", "acc", "muscle_x", "steps"):
+        assert torch.equal(getattr(a, k), getattr(b, k)), k
+
+
+def test_state_setters_write_through_permuted_batch():
+    """the state properties of a permuted (ragged) batch are gathered copies; assignment scatters the
+    caller-order values into the stored order."""
+    import torch
+    from walker_gym_amd.batched_env import BatchedPhysicsEnv
+    from walker_gym_amd.synthetic import ragged_walkers
+    env = BatchedPhysicsEnv(ragged_walkers(300, seed=81, mmin=3, mmax=30), device="cuda:0", in3d=1)
+    assert env.batch.row is not None
+    for k in ("pos", "vel", "acc", "muscle_x"):
+        want = torch.rand_like(getattr(env, k))
+        setattr(env, k, want)
+        assert torch.equal(getattr(env, k), want), k

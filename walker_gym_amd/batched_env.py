@@ -123,7 +123,7 @@ class BatchedPhysicsEnv:
         self.params = EnvParams(**params)
         self.sigma = float(rand_sigma)
         host = spec_or_layout if isinstance(spec_or_layout, HostLayout) else pack(spec_or_layout)
-        self.batch = DeviceBatch(host, device, contact=contact)
+        self.batch = DeviceBatch(host, device, contact=contact, wave_ok=self._wave_ok())
         if int(self.params.pair_mode) & 4:
             self.batch.enable_radius()
         self.device = device
@@ -202,8 +202,26 @@ class BatchedPhysicsEnv:
             self._alloc_outputs()
         if int(self.params.pair_mode) & 4:
             self.batch.enable_radius()
+        if self._needs_plan() and self.batch.wave_ok != self._wave_ok():
+            self.batch.replan(self._wave_ok())   # the plan kind follows the parameters (DeviceBatch.replan)
         self._pstruct = self.params.to_struct()
         self._generation += 1   # graphs captured before this replay stale parameters: WalkerGraph refuses them
+
+    def _wave_ok(self) -> bool:
+        """The parameters can run on the barrier-free wave kernels (engine.py springs, no pair forces)."""
+        return int(self.params.spring_mode) == 0 and int(self.params.pair_mode) == 0
+
+    def _needs_plan(self) -> bool:
+        """Batches whose launch plan depends on the parameters: ragged, or uniform with M not dividing 64."""
+        M = self.batch.M
+        return bool(self.batch.host.ragged) or not (4 <= M <= 64 and 64 % M == 0)
+
+    def resident_ok(self) -> bool:
+        """wg_rollout keeps the walkers in registers across steps (one launch for every step) for this batch and
+        these parameters: uniform, M | 64, engine.py springs, no pair forces (otherwise it steps like wg_step)."""
+        M = self.batch.M
+        return (not self.batch.ragged and 4 <= M <= 64 and 64 % M == 0 and self._wave_ok()
+                and os.environ.get("WG_LEAN", "1") != "0")
 
     def _check_action(self, action):
         if action is None:
@@ -219,8 +237,15 @@ class BatchedPhysicsEnv:
 
     # ------------------------------------------------------------------ API
     def step(self, action=None):
-        """One env step for all walkers: act -> physics -> run1 -> obs/reward/done/info (one launch)."""
+        """One env step for all walkers: act -> physics -> run1 -> obs/reward/done/info: one launch per walker range
+        (the default ranges, joined on the calling stream before this returns its outputs)."""
         act, cols = self._check_action(action)
+        lanes = self._lanes(None)
+        if act is not None and lanes > 1:
+            self._run_lanes(act[None], 1, lambda w0, w1: self._outputs(
+                self.obs[w0:w1], self.reward[w0:w1], self.done[w0:w1], self.centroid[w0:w1], self.energy[w0:w1],
+                pad_clean=True), lanes)
+            return self.obs, self.reward, self.done.bool(), self.info()
         L = _lib.load()
         o = self._outputs(self.obs, self.reward, self.done, self.centroid, self.energy, pad_clean=True)
         _lib.check(L.wg_step(C.byref(self.batch.struct), C.byref(self._pstruct),
@@ -251,7 +276,8 @@ class BatchedPhysicsEnv:
         require_tensor(done_out, "done_out", dv, torch.uint8, (T, self.N))
         # one resident launch holds its walkers for all T steps: no per-step launch tail for a second range to fill
         # (profiles/r02_ab_resident_occupancy.json: 38.2 us/step with one range, 39.6 with two)
-        lanes = self._lanes(1 if (resident and lanes is None) else lanes) if T > 0 else 1
+        # (only where the resident kernel actually runs: otherwise the default walker ranges keep their overlap)
+        lanes = self._lanes(1 if (resident and lanes is None and self.resident_ok()) else lanes) if T > 0 else 1
         entry = "wg_rollout" if resident else "wg_step"
         if lanes > 1:
             self._run_lanes(actions, T, lambda w0, w1: self._outputs(
@@ -277,7 +303,7 @@ class BatchedPhysicsEnv:
         T, n, cols = actions.shape
         if n != self.N or T not in (1, n_steps):
             raise ValueError("actions must be a contiguous [n_steps or 1, N, A] device tensor")
-        lanes = self._lanes(1 if (resident and lanes is None) else lanes)
+        lanes = self._lanes(1 if (resident and lanes is None and self.resident_ok()) else lanes)
         entry = "wg_rollout" if resident else "wg_step"
         if lanes > 1:
             return self._run_lanes(actions, int(n_steps), lambda w0, w1: self._outputs(
@@ -405,23 +431,45 @@ class BatchedPhysicsEnv:
     def info(self) -> dict:
         return {"steps": self.batch.caller("steps"), "centroid_position": self.centroid, "total_energy": self.energy}
 
-    # state accessors in the caller's order: live views into the batch, or gathered copies for a ragged batch
-    # (stored in wave-tile / size order; write through batch.to_stored / batch.stored_mass)
+    # state accessors in the caller's order.  An unpermuted batch returns live views into its tensors; a ragged batch
+    # (stored in wave-tile / size order) returns gathered COPIES, so in-place writes into them do not reach the batch:
+    # assign instead (env.pos = t, env.vel[...] edits then env.vel = edited), which scatters into the stored order.
+    def _set_state(self, name: str, value) -> None:
+        dst = getattr(self.batch, name)
+        t = torch.as_tensor(value, dtype=dst.dtype).to(self.device).reshape(dst.shape)
+        dst.copy_(self.batch.to_stored(self.batch.KIND[name], t))
+
     @property
     def pos(self):
         return self.batch.caller("pos")
+
+    @pos.setter
+    def pos(self, value):
+        self._set_state("pos", value)
 
     @property
     def vel(self):
         return self.batch.caller("vel")
 
+    @vel.setter
+    def vel(self, value):
+        self._set_state("vel", value)
+
     @property
     def acc(self):
         return self.batch.caller("acc")
 
+    @acc.setter
+    def acc(self, value):
+        self._set_state("acc", value)
+
     @property
     def muscle_x(self):
         return self.batch.caller("muscle_x")
+
+    @muscle_x.setter
+    def muscle_x(self, value):
+        self._set_state("muscle_x", value)
 
     @property
     def contact(self):

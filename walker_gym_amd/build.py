@@ -19,6 +19,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "walker_hip.hip")
 HDR = os.path.join(ROOT, "include", "walker_hip.h")
+POWF2 = os.path.join(HERE, "csrc", "powf2.h")
 OUT = os.path.join(HERE, "libwalker_hip.so")
 ARCH = os.environ.get("WALKER_HIP_ARCH", "gfx950")
 
@@ -42,7 +43,7 @@ def needs_build(out: str = OUT) -> bool:
     if not os.path.exists(out):
         return True
     t = os.path.getmtime(out)
-    return any(os.path.getmtime(p) > t for p in (SRC, HDR, __file__))
+    return any(os.path.getmtime(p) > t for p in (SRC, HDR, POWF2, __file__))
 
 
 def build(force: bool = False, verbose: bool = False) -> str:

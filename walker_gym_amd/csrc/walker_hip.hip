@@ -30,6 +30,7 @@
 #include <cstring>
 
 #include "walker_hip.h"
+#include "powf2.h"
 
 namespace {
 
@@ -64,7 +65,8 @@ struct KParams {
     double g;
     int max_steps, midform, conmid, spring_mode, action_mode;
     int integrator; // 2: Point.run2, otherwise Point.run1
-    int pair_mode;  // bitmask (lean kernel): 1 Point.gravity, 2 Point.coulomb, 4 Point.bounce, after the springs
+    int pair_mode;  // bitmask, after the springs in bit order: 1 Point.gravity, 2 Point.coulomb, 4 Point.bounce,
+                    // 8 G2 Point.gravity (gravity_vec: zero a, float32 pairs), 16 Point.electrostatic (every point)
     double pair_g, pair_k, pair_e;
     float bounce_kh;  // float32(k / 2) of Point.bounce(k)
     // spring_mode 2, the G3 engine (gym/optimized_walker/env.py:135-184), everything rounded to float32
@@ -285,6 +287,15 @@ __device__ __forceinline__ float sqrt_mid(float s) {
     const float rd = __uint_as_float(__float_as_uint(r) - 1u), ru = __uint_as_float(__float_as_uint(r) + 1u);
     float o = (__builtin_fmaf(-rd, r, s) <= 0.f) ? rd : r;
     return (__builtin_fmaf(-ru, r, s) > 0.f) ? ru : o;
+}
+
+// numpy's float32 `x ** 2` (a scalar power: libm powf, not x*x; powf2.h): RN(x*x) unless x*x lies within 2^-32 of a
+// float rounding boundary (0.29 % of floats), then glibc's algorithm restated (cold, only the lanes that need it)
+__device__ __attribute__((noinline)) float np_sq_cold(float x) { return pw_pow2(x); }
+__device__ __forceinline__ float np_sq(float x) {
+    float f;
+    if (__builtin_expect(!pw_pow2_fast(x, &f), 0)) f = np_sq_cold(x);
+    return f;
 }
 
 // Global -> LDS copy of n 4-byte words (16-B vector loads when both ends allow it).
@@ -744,10 +755,65 @@ __device__ __forceinline__ void bounce_term(float cur, float nf, float d0, float
     az = (float)((double)az + ddiv_f32d(t2, md, ym));
 }
 
+// One partner of G2 Point.gravity = Point.gravity_vec (gym/optimized_engine.py:167-193, the N-body of the performance_demo
+// loop, gym/performance_demo.py:52-58), seen from mass q, all float32 as numpy evaluates it: distance =
+// norm(p_j - p_i) WITHOUT .astype(float) (:185-186: a numpy float32); max(distance, Config.r); f = -Config.g * m_i * m_j
+// / distance ** 2 (:189: the Python-float numerator weakly cast to float32, distance ** 2 numpy's float32 power =
+// libm powf, np_sq); force = f * direction / distance (:192, float32); p_i.forced(force), p_j.forced(-force)
+// (:193-194, a += force / m in float32).  d = partner - self: q receives (f * d) / distance from either role (the
+// negations are exact).  cg = f32(-Config.g * m_lo * m_hi) from the Python product (numerator in float64).  A
+// distance below Config.r leaves the Python float 16e-36 in its place: f and the division then go through its
+// float32 casts (:189-192 with a Python-float distance).
+__device__ __forceinline__ void g2_gravity_term(double cgd, float d0, float d1, float d2, float mf, float &ax,
+                                                float &ay, float &az) {
+    const float dist = np_norm3(d0, d1, d2);
+    float f, dv;
+    if (__builtin_expect(!(CONFIG_R > (double)dist), 1)) {   // unclamped (NaN too: max keeps the float32 NaN)
+        f = (float)cgd / np_sq(dist);
+        dv = dist;
+    } else {
+        f = (float)(cgd / (CONFIG_R * CONFIG_R));              // Python floats throughout, cast where they meet float32
+        dv = (float)CONFIG_R;
+    }
+    ax = ax + ((f * d0) / dv) / mf;
+    ay = ay + ((f * d1) / dv) / mf;
+    az = az + ((f * d2) / dv) / mf;
+}
+
 // ------------------------------------------------------------------ pair passes from LDS (workgroup kernel)
 // SURVEY §8(f) 3 for walkers the lean kernel does not take (M not dividing 64, M > 64, ragged batches): the
 // arithmetic of pair_central / pair_bounce (lean kernel, below) with the partners' positions read from the tile's
 // LDS copy, unchanged until every mass of the tile has accumulated (walker_step_kernel puts a barrier there).
+// Point.electrostatic (gym/engine.py:150-158) of mass q: for every other point i in registry order, r = max(norm(p_q -
+// p_i) as float64, Config.r), f = -Config.k * e_q * e_i / r**2 (self's charge first, unlike coulomb's lower index
+// first), then q.anti_forced(f, i): only q receives, (-f) * (p_i - p_q) / r in float64, divided by m.  The same
+// partner arithmetic as the coulomb pass (exact fast form, IEEE redo when flagged).
+__device__ void pair_electrostatic_lds(const wg_batch &b, const KParams &kp, const float *spos, int lm, int M, int q,
+                                       size_t g0, double md, double ym, float &ax, float &ay, float &az) {
+    const float *p3 = spos + 3 * (lm + q);
+    const double sq = b.charge ? b.charge[g0 + q] : kp.pair_e;
+    const float sx = ax, sy = ay, sz = az;
+    bool bad = !WG_FAST_PAIR;
+    if (WG_FAST_PAIR) {
+        for (int pj = 0; pj < M; pj++) {
+            if (pj == q) continue;
+            const float *o3 = spos + 3 * (lm + pj);
+            const double os = b.charge ? b.charge[g0 + pj] : kp.pair_e;
+            pair_central_fast(kp.pair_k, sq, os, o3[0] - p3[0], o3[1] - p3[1], o3[2] - p3[2], md, ym, ax, ay, az, bad);
+        }
+        bad = bad || !__builtin_isfinite(ax + ay + az);
+    }
+    if (__builtin_expect(bad, 0)) {
+        ax = sx; ay = sy; az = sz;
+        for (int pj = 0; pj < M; pj++) {
+            if (pj == q) continue;
+            const float *o3 = spos + 3 * (lm + pj);
+            const double os = b.charge ? b.charge[g0 + pj] : kp.pair_e;
+            pair_central_term(kp.pair_k, sq, os, o3[0] - p3[0], o3[1] - p3[1], o3[2] - p3[2], md, ym, ax, ay, az);
+        }
+    }
+}
+
 // Mass q of the walker whose masses are LDS [lm, lm + M) and global [g0, g0 + M).
 __device__ void pair_forces_lds(const wg_batch &b, const KParams &kp, const float *spos, const float *sm, int lm,
                                 int M, int q, size_t g0, float mf, float &ax, float &ay, float &az) {
@@ -803,6 +869,18 @@ __device__ void pair_forces_lds(const wg_batch &b, const KParams &kp, const floa
             }
         }
     }
+    if ((kp.pair_mode & 8) && M >= 2) {      // G2 Point.gravity: every a zeroed first (optimized_engine.py:174-175)
+        ax = 0.f; ay = 0.f; az = 0.f;
+        for (int pj = 0; pj < M; pj++) {
+            if (pj == q) continue;
+            const float *o3 = spos + 3 * (lm + pj);
+            const double mo = (double)sm[lm + pj];
+            g2_gravity_term(((-kp.pair_g) * (pj < q ? mo : md)) * (pj < q ? md : mo), o3[0] - p3[0], o3[1] - p3[1],
+                            o3[2] - p3[2], mf, ax, ay, az);
+        }
+    }
+    if (kp.pair_mode & 16)                   // Point.electrostatic (gym/engine.py:150-158) of every point
+        pair_electrostatic_lds(b, kp, spos, lm, M, q, g0, md, ym, ax, ay, az);
 }
 
 // ------------------------------------------------------------------ the step kernel
@@ -1009,7 +1087,7 @@ __global__ __launch_bounds__(MAXT) void walker_step_kernel(
             }
             // reduction terms of the new state: |v|, m*|v|^2, f32(m*g)*(y-ground)
             nv = np_norm3(vx, vy, vz);
-            ke = mf * (nv * nv);   // numpy's float32 ** 2 is libm powf: may differ by 1 ulp
+            ke = mf * np_sq(nv);   // p.m * norm(p.v) ** 2 (gym/optimized_env.py:242)
             pe = (float)(md * kp.g) * (py - kp.ground);
             if (!SHFL) { s.nrm[lp] = nv; s.ke[lp] = ke; s.pe[lp] = pe; }
         }
@@ -1025,7 +1103,7 @@ __global__ __launch_bounds__(MAXT) void walker_step_kernel(
                 ax = s.acc[3 * lp]; ay = s.acc[3 * lp + 1]; az = s.acc[3 * lp + 2];
             }
             nv = np_norm3(vx, vy, vz);
-            ke = mf * (nv * nv);
+            ke = mf * np_sq(nv);
             pe = (float)((double)mf * kp.g) * (py - kp.ground);
             if (!SHFL) { s.nrm[lp] = nv; s.ke[lp] = ke; s.pe[lp] = pe; }
         }
@@ -1423,8 +1501,10 @@ __device__ __forceinline__ double lane_gather_d(double v, int src_byte) {
 // force = (-f * (p_partner - p_q)) / r, all float64 (f is a numpy float64 scalar, r came from .astype(float));
 // forced (:65-67): a = f32(f64(a) + force/m).  Every lane runs the loop (partner state by ds_bpermute);
 // non-mass lanes discard theirs.  IEEE float64 divisions: an opt-in mode, not the headline path.
+// self_first (Point.electrostatic, gym/engine.py:150-158): f = -Config.k * e_q * e_partner for every partner (self's
+// charge first) instead of the lower index's first.
 __device__ __forceinline__ void pair_central(double coef, double sq, const float *p3, float mf, int lane, int M,
-                                             bool is_mass, float &ax, float &ay, float &az) {
+                                             bool is_mass, float &ax, float &ay, float &az, bool self_first = false) {
     const int gb = lane & ~(M - 1), q = lane & (M - 1);
     const double md = (double)mf, ym = 1.0 / md;
     const float sx = ax, sy = ay, sz = az;
@@ -1436,7 +1516,8 @@ __device__ __forceinline__ void pair_central(double coef, double sq, const float
             const double os = lane_gather_d(sq, src);
             if (!is_mass || pj == q) continue;
             const float d0 = ox - p3[0], d1 = oy - p3[1], d2 = oz - p3[2];   // partner - self
-            pair_central_fast(coef, pj < q ? os : sq, pj < q ? sq : os, d0, d1, d2, md, ym, ax, ay, az, bad);
+            const bool lo = pj < q && !self_first;
+            pair_central_fast(coef, lo ? os : sq, lo ? sq : os, d0, d1, d2, md, ym, ax, ay, az, bad);
         }
         bad = is_mass && (bad || !__builtin_isfinite(ax + ay + az));
     }
@@ -1449,7 +1530,8 @@ __device__ __forceinline__ void pair_central(double coef, double sq, const float
             const double os = lane_gather_d(sq, src);
             if (!bad || pj == q) continue;
             const float d0 = ox - p3[0], d1 = oy - p3[1], d2 = oz - p3[2];
-            pair_central_term(coef, pj < q ? os : sq, pj < q ? sq : os, d0, d1, d2, md, ym, cx, cy, cz);
+            const bool lo = pj < q && !self_first;
+            pair_central_term(coef, lo ? os : sq, lo ? sq : os, d0, d1, d2, md, ym, cx, cy, cz);
         }
         if (bad) { ax = cx; ay = cy; az = cz; }
     }
@@ -1484,6 +1566,24 @@ __device__ __forceinline__ void pair_bounce(float kh, double rs, const float *p3
     }
 }
 
+// pair_mode bit 8: G2 Point.gravity (gravity_vec, g2_gravity_term) over the walker's M lanes: every a zeroed first
+// (gym/optimized_engine.py:174-175; the walker has M >= 4 masses here), partners in ascending order by ds_bpermute.
+__device__ __forceinline__ void pair_g2_gravity(double g, const float *p3, float mf, int lane, int M, bool is_mass,
+                                                float &ax, float &ay, float &az) {
+    const int gb = lane & ~(M - 1), q = lane & (M - 1);
+    const double md = (double)mf;
+    ax = 0.f; ay = 0.f; az = 0.f;
+    for (int pj = 0; pj < M; pj++) {
+        const int src = (gb + pj) << 2;
+        const float ox = lane_gather(p3[0], src), oy = lane_gather(p3[1], src), oz = lane_gather(p3[2], src);
+        const float om = lane_gather(mf, src);
+        if (!is_mass || pj == q) continue;
+        const double mo = (double)om;
+        g2_gravity_term(((-g) * (pj < q ? mo : md)) * (pj < q ? md : mo), ox - p3[0], oy - p3[1], oz - p3[2], mf, ax,
+                        ay, az);
+    }
+}
+
 // The pair passes of one wave (pair_mode != 0): gravity, coulomb, bounce, each over every walker of the wave.
 // Per-mass charges / radii are loaded here, not in lean_load, so the default path carries no extra registers.
 __device__ __forceinline__ void pair_forces(const wg_batch &b, const KParams &kp, const float *p3, float mf,
@@ -1497,6 +1597,11 @@ __device__ __forceinline__ void pair_forces(const wg_batch &b, const KParams &kp
     if (kp.pair_mode & 4) {
         const double rs = is_mass ? b.radius[pl] : 0.0;
         pair_bounce(kp.bounce_kh, rs, p3, mf, lane, M, is_mass, ax, ay, az);
+    }
+    if (kp.pair_mode & 8) pair_g2_gravity(kp.pair_g, p3, mf, lane, M, is_mass, ax, ay, az);
+    if (kp.pair_mode & 16) {
+        const double e = (b.charge && is_mass) ? b.charge[pl] : kp.pair_e;
+        pair_central(kp.pair_k, e, p3, mf, lane, M, is_mass, ax, ay, az, true);
     }
 }
 
@@ -1609,12 +1714,13 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
         mass_accumulate<LeanTerms, !RES>(ts, reinterpret_cast<const uint16_t *>(s_inc) + 2 * lb, lb, L.io0, r1, mf, ax,
                                          ay, az, 0);
     }
-    if (kp.pair_mode) pair_forces(b, kp, L.p3, mf, pl, lane, M, is_mass, ax, ay, az);   // every lane (gathers)
+    // every lane (gathers); the resident kernel runs pair-free batches only (wg_rollout falls back to wg_step)
+    if (!RES && kp.pair_mode) pair_forces(b, kp, L.p3, mf, pl, lane, M, is_mass, ax, ay, az);
     if (is_mass) {
         mass_tail(kp, mf, (float)ym, L.p3, L.v3, px, py, pz, vx, vy, vz, ax, ay, az, hit, pin);
         if (b.radius && store) b.radius[pl] = hit ? 3.0 : 1.0;   // p.r = 3 / p.r = 1 (gym/optimized_env.py:156,175)
         nv = np_norm3(vx, vy, vz);
-        ke = mf * (nv * nv);   // numpy's float32 ** 2 is libm powf: may differ by 1 ulp
+        ke = mf * np_sq(nv);   // p.m * norm(p.v) ** 2 (gym/optimized_env.py:242)
         pe = (float)((double)mf * kp.g) * (py - kp.ground);
     }
     STAMP(4);
@@ -1985,7 +2091,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
         const float nv = nvm;
         s_tp[3 * lane] = px; s_tp[3 * lane + 1] = py; s_tp[3 * lane + 2] = pz;
         s_tn[lane] = nv;
-        s_tk[lane] = mf * (nv * nv);   // numpy's float32 ** 2 is libm powf: may differ by 1 ulp
+        s_tk[lane] = mf * np_sq(nv);   // p.m * norm(p.v) ** 2 (gym/optimized_env.py:242)
         s_te[lane] = (float)((double)mf * kp.g) * (py - kp.ground);
     }
     wave_sync();
@@ -2445,8 +2551,9 @@ int run(const wg_batch *b, const wg_params *p, const float *action, int32_t cols
                            rag_geo(b, out.obs ? out.obs_stride : 0, &rgeo);
     if (p->spring_mode < 0 || p->spring_mode > 2)
         return fail(WG_EINVAL, "spring_mode %d: 0 (engine.py), 1 (G2 element), 2 (G3 engine) only", p->spring_mode);
-    if (step && (p->pair_mode & ~7))
-        return fail(WG_EINVAL, "pair_mode %d: bits 1 (gravity), 2 (coulomb), 4 (bounce) only", p->pair_mode);
+    if (step && (p->pair_mode & ~31))
+        return fail(WG_EINVAL, "pair_mode %d: bits 1 (gravity), 2 (coulomb), 4 (bounce), 8 (G2 gravity_vec), "
+                               "16 (electrostatic) only", p->pair_mode);
     if (step && p->pair_mode != 0 && p->spring_mode != 0)
         return fail(WG_EINVAL, "pair_mode %d needs spring_mode 0", p->pair_mode);
     if (step && (p->pair_mode & 4) && !b->radius)

@@ -34,7 +34,7 @@ class DeviceBatch:
 
     STATE = ("pos", "vel", "acc", "muscle_x", "steps")   # + radius when kept (Point.bounce)
 
-    def __init__(self, host: HostLayout, device: torch.device, contact: bool = True):
+    def __init__(self, host: HostLayout, device: torch.device, contact: bool = True, wave_ok: bool = True):
         if device.type != "cuda":
             raise ValueError("DeviceBatch needs a ROCm device (torch 'cuda' device); there is no CPU path")
         self.host = host
@@ -74,10 +74,23 @@ class DeviceBatch:
         self.plan = None
         self.plan_blocks = 0
         self.ragged_kind = 0
-        L = _lib.load()
+        self.replan(wave_ok)
+
+    def replan(self, wave_ok: bool) -> None:
+        """Choose the launch plan for parameters that can (wave_ok) or cannot use the barrier-free wave kernel.
+        wave_ok (spring_mode 0, no pair forces): a uniform batch the lean kernel does not take (M not dividing 64)
+        becomes wave tiles of whole walkers (identity order), a ragged batch whose walkers each fit one wave gets
+        wave tiles.  Otherwise the workgroup kernel runs, on its own plan: uniform workgroup tiles (uniform_geo packs
+        e.g. 19 M = 13 walkers per 256 lanes) or wg_plan_ragged tiles — a wave plan would leave it at most 64 masses
+        per workgroup, 3/4 of the lanes idle (pair forces, the G2 element, the G3 engine)."""
+        host, L = self.host, _lib.load()
+        self.wave_ok = bool(wave_ok)
         lean_shape = 4 <= self.M <= 64 and 64 % self.M == 0
-        if (not self.ragged and not lean_shape and self.A <= 64 and L.wg_wave_edge_passes(self.M, self.K) > 0
-                and os.environ.get("WG_UNIFORM_WAVES", "1") != "0"):
+        self.ragged = host.ragged
+        self.plan, self.plan_blocks, self.ragged_kind = None, 0, 0
+        waves = (wave_ok and self.A <= 64 and L.wg_wave_edge_passes(self.M, self.K) > 0
+                 and os.environ.get("WG_LEAN", "1") != "0")
+        if (not self.ragged and not lean_shape and waves and os.environ.get("WG_UNIFORM_WAVES", "1") != "0"):
             # a uniform batch the lean kernel does not take (M not dividing 64): stepped as wave tiles of whole
             # walkers (the barrier-free wave kernel; identity order) instead of workgroup tiles
             self.ragged = True
@@ -86,11 +99,11 @@ class DeviceBatch:
             args = (host.mass_off.ctypes.data_as(C.c_void_p), host.edge_off.ctypes.data_as(C.c_void_p),
                     host.muscle_off.ctypes.data_as(C.c_void_p), self.N, plan.ctypes.data_as(C.c_void_p), self.N + 1)
             # wave tiles when every walker fits one wave (the wave kernel), workgroup tiles otherwise
-            if L.wg_wave_edge_passes(self.M, self.K) > 0 and self.A <= 64:
+            if waves:
                 nb, self.ragged_kind = _lib.check(L.wg_plan_waves(*args), "wg_plan_waves"), 2
             else:
                 nb, self.ragged_kind = _lib.check(L.wg_plan_ragged(*args), "wg_plan_ragged"), 1
-            self.plan = _to_dev(plan[:nb + 1], dv)
+            self.plan = _to_dev(plan[:nb + 1], self.device)
             self.plan_blocks = nb
         self.struct = self._make_struct()
 
@@ -101,22 +114,22 @@ class DeviceBatch:
         t = getattr(self, name)
         if t is None or not self._perm:
             return t
-        kind = {"pos": "mass", "vel": "mass", "acc": "mass", "contact": "mass", "radius": "mass",
-                "muscle_x": "muscle", "steps": "walker"}[name]
-        return t.index_select(0, self._perm[kind])
+        return t.index_select(0, self._perm[self.KIND[name]])
 
     def stored_mass(self, q: int) -> int:
         """Stored index of the caller's mass q."""
         return int(self.host.mass_perm[q]) if self._perm else int(q)
 
     def to_stored(self, kind: str, t: torch.Tensor) -> torch.Tensor:
-        """A per-mass ('mass') or per-walker ('walker') caller-order tensor in the stored order."""
+        """A per-mass ('mass'), per-muscle ('muscle') or per-walker ('walker') caller-order tensor in the stored order."""
         if not self._perm:
             return t
         if kind == "walker":
             return t.index_select(0, self._perm["row"])
+        if kind not in ("mass", "muscle"):
+            raise ValueError(f"to_stored: kind must be 'mass', 'muscle' or 'walker', not {kind!r}")
         out = torch.empty_like(t)
-        out.index_copy_(0, self._perm["mass"], t)
+        out.index_copy_(0, self._perm[kind], t)
         return out
 
     def enable_radius(self) -> None:
@@ -184,15 +197,22 @@ class DeviceBatch:
             geo["wave_tiles"] = self.plan_blocks
         return geo
 
+    KIND = {"pos": "mass", "vel": "mass", "acc": "mass", "contact": "mass", "radius": "mass", "muscle_x": "muscle",
+            "steps": "walker"}
+
     def state_dict(self) -> dict:
-        sd = {k: getattr(self, k).clone() for k in self.STATE}
+        """The walker state in the CALLER's walker / mass / muscle order, whatever order the batch is stored in (a
+        ragged batch is stored in wave-tile or size order, which depends on the batch and on WG_TILE_ORDER): a dict
+        saved under one storage order loads correctly under another."""
+        sd = {k: self.caller(k).clone() for k in self.STATE}
         if self.radius is not None:
-            sd["radius"] = self.radius.clone()
+            sd["radius"] = self.caller("radius").clone()
         return sd
 
     def load_state_dict(self, sd: dict) -> None:
+        """Inverse of state_dict: caller-order tensors copied into the stored order."""
         for k in self.STATE:
-            getattr(self, k).copy_(sd[k])
+            getattr(self, k).copy_(self.to_stored(self.KIND[k], sd[k].to(self.device)))
         if "radius" in sd:
             self.enable_radius()
-            self.radius.copy_(sd["radius"])
+            self.radius.copy_(self.to_stored("mass", sd["radius"].to(self.device)))

@@ -351,7 +351,13 @@ def main():
         B = bytes_per_walker_step(env.batch.host, bool(params.get("in3d")))
         M, K = env.batch.M, env.batch.K
         uniform = not env.batch.ragged
-        B_layout = layout_bytes_per_walker_step(M, K, env.batch.A, D) if uniform else None
+        if uniform:
+            B_layout = layout_bytes_per_walker_step(M, K, env.batch.A, D)
+        else:   # per walker (its own M, K, A and obs row), averaged; the buffer-by-buffer account is DESIGN §4
+            hm = env.batch.host
+            Mw, Kw, Aw = np.diff(hm.mass_off), np.diff(hm.edge_off), np.diff(hm.muscle_off)
+            B_layout = round(float(np.mean(layout_bytes_per_walker_step(
+                Mw, Kw, Aw, (9 if params.get("in3d") else 6) * Mw + Aw, ragged=True))), 1)
         tr = load_traffic(args.workload, N)
         geo = env.launch_geometry()
         head_ms = single_ms if single_ms is not None else step_ms

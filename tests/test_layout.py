@@ -183,3 +183,26 @@ def test_wave_tile_order_caps_and_reproduction_edge_cases():
         # the lower bound on tiles from masses alone is met within a tile or two where masses bind
         if Ks.max() == 0:
             assert nb == -(-len(Ms) // 32)
+
+
+def test_wave_tile_order_windows_keep_caller_locality():
+    """Windowed best-fit packing (layout.wave_tile_order, WG_TILE_WINDOW): each window of W consecutive caller
+    walkers occupies W consecutive stored positions (so its wave tiles are consecutive and, under the kernel's
+    XCD-aware workgroup order, share one L2), at almost the tile count of one global packing."""
+    from walker_gym_amd.layout import wave_edge_passes, wave_tile_order
+    spec = ragged_walkers(5000, seed=17, mmin=4, mmax=32)
+    M, K = np.diff(spec["mass_off"]), np.diff(spec["edge_off"])
+    A = np.asarray(spec["n_muscles"])
+    ne = wave_edge_passes(int(M.max()), int(K.max()))
+
+    def ntiles(order):
+        n, P, E, U, c = 1, 0, 0, 0, 0
+        for w in order:
+            if c and (P + M[w] > 64 or E + K[w] > 64 * ne or U + A[w] > 64 or c + 1 > 32):
+                n, P, E, U, c = n + 1, 0, 0, 0, 0
+            P, E, U, c = P + M[w], E + K[w], U + A[w], c + 1
+        return n
+    glob, win = wave_tile_order(M, K, A, ne, window=0), wave_tile_order(M, K, A, ne, window=512)
+    for s in range(0, 5000, 512):
+        assert sorted(win[s:s + 512].tolist()) == list(range(s, min(s + 512, 5000)))
+    assert ntiles(win) <= 1.01 * ntiles(glob), (ntiles(win), ntiles(glob))

@@ -9,7 +9,8 @@ from conftest import GOLDEN
 
 
 @pytest.mark.parametrize("name,T", [("balance_3d", 100), ("canonical", 30), ("box_3d", 30), ("ragged", 20),
-                                    ("pair_gravity_canonical", 20)])
+                                    ("pair_gravity_canonical", 20), ("perfdemo_chain_10", 40),
+                                    ("pair_g2_gravity_canonical", 20)])
 def test_refstyle_matches_golden(name, T):
     from oracle.oracle import spec_from_npz
     from oracle.refstyle import walkers
@@ -17,7 +18,7 @@ def test_refstyle_matches_golden(name, T):
     spec, params = spec_from_npz(z)
     ws = walkers(spec, params)
     for t in range(T):
-        res = [wk.step(z["actions"][t, w]) for w, wk in enumerate(ws)]
+        res = [wk.step(z["actions"][t, w] if z["actions"].shape[2] else []) for w, wk in enumerate(ws)]
         pos = np.array([p.pos for wk in ws for p in wk.phys])
         np.testing.assert_array_equal(pos, z["out_pos"][t])
         for w, (obs, rew, done, info) in enumerate(res):

@@ -75,7 +75,17 @@ struct KParams {
     int friction_mode;   // 0: (-v)*(|deep|*friction) (gym/optimized_env.py:168-172); 1: (v*deep)*friction (gym/env.py:41)
     int prio;         // WG_LEAN_PRIO: 1 (default) raise the wave priority while a lean tile issues its loads, so a
                       // wave's HBM requests leave before other waves' arithmetic; 0 off
+    int xcd;          // WG_XCD bitmask: XCD-aware workgroup order (xcd_block) for 1 the wave kernel, 2 the lean kernel
 };
+
+// XCD-aware workgroup order: MI355X deals workgroups round-robin over its 8 XCDs (each with its own L2; observed
+// placement, speed only), so hardware block b runs on XCD group b % 8.  The guide's bijective T1 swizzle maps b to a
+// logical block so that each XCD group takes one contiguous run of logical blocks, in launch order: consecutive
+// tiles then share an L2 (their partial output lines merge there and their shared input lines are fetched once).
+__device__ __forceinline__ int xcd_block(int bid, int nwg) {
+    const int q = nwg >> 3, r = nwg & 7, x = bid & 7;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+}
 
 // Per-launch geometry: caps of one workgroup's slice (LDS carve sizes).
 struct Geo {
@@ -485,17 +495,20 @@ __device__ __forceinline__ void mass_tail(const KParams &kp, float mf, float ymf
         env_forces<false>(kp, mf, ymf, vx, vy, vz, py, ax, ay, az, hit);
     }
     if (pinned) { ax = 0.f; ay = 0.f; az = 0.f; }   // DingPoint.forced is a no-op: a stays zeros()
-    // v += a*t in both integrators; the position update differs.  Both forms are computed and one selected:
-    // an if/else over px..vz references made hipcc keep them in a dynamically indexed stack array (scratch).
+    // v += a*t in both integrators; the position update differs (a wave-uniform branch on the parameter, on
+    // scalar locals: an if/else over px..vz references had made hipcc keep them in a stack array)
     const float nvx = vx + ax * kp.dt, nvy = vy + ay * kp.dt, nvz = vz + az * kp.dt;
-    // Point.run1 (gym/engine.py:174-178): pos += v_new*t
-    const float p1x = px + nvx * kp.dt, p1y = py + nvy * kp.dt, p1z = pz + nvz * kp.dt;
-    // Point.run2 (gym/engine.py:184-187): pos += v*t + 0.5*a*t**2 (numpy: (v*t) + ((0.5*a)*f32(t**2)))
-    const float p2x = px + (vx * kp.dt + (0.5f * ax) * kp.dt2);
-    const float p2y = py + (vy * kp.dt + (0.5f * ay) * kp.dt2);
-    const float p2z = pz + (vz * kp.dt + (0.5f * az) * kp.dt2);
-    const bool run2 = kp.integrator == 2;
-    px = run2 ? p2x : p1x; py = run2 ? p2y : p1y; pz = run2 ? p2z : p1z;
+    float dpx, dpy, dpz;
+    if (__builtin_expect(kp.integrator == 2, 0)) {
+        // Point.run2 (gym/engine.py:184-187): pos += v*t + 0.5*a*t**2 (numpy: (v*t) + ((0.5*a)*f32(t**2)))
+        dpx = vx * kp.dt + (0.5f * ax) * kp.dt2;
+        dpy = vy * kp.dt + (0.5f * ay) * kp.dt2;
+        dpz = vz * kp.dt + (0.5f * az) * kp.dt2;
+    } else {
+        // Point.run1 (gym/engine.py:174-178): pos += v_new*t
+        dpx = nvx * kp.dt; dpy = nvy * kp.dt; dpz = nvz * kp.dt;
+    }
+    px = px + dpx; py = py + dpy; pz = pz + dpz;
     vx = nvx; vy = nvy; vz = nvz;
 }
 
@@ -646,8 +659,22 @@ __device__ inline float seq_chain(float x, int M) {
     for (int t = 1; t < M; t++) a = dpp_f<CTRL>(a) + x;
     return a;
 }
+// M == 4 (Balance-v0, Box-v0): a walker is one DPP quad, so every lane of it adds the quad's four values in order
+// from quad_perm broadcasts: ((0 + x_0) + x_1) + x_2) + x_3 in every lane, no LDS round trip (the step of a small
+// batch is one wave's latency chain).
+template <int K> __device__ inline float quad_bcast(float v) { return dpp_f<K | (K << 2) | (K << 4) | (K << 6)>(v); }
+__device__ inline float seq_sum_quad(float x) {
+    float a = 0.f + quad_bcast<0>(x);
+    a = a + quad_bcast<1>(x);
+    a = a + quad_bcast<2>(x);
+    return a + quad_bcast<3>(x);
+}
 __device__ inline void seq_sum3_lanes(float x, float y, float z, int base, int M, float &sx, float &sy, float &sz) {
     float a, b, c;
+    if (M == 4) {
+        sx = seq_sum_quad(x); sy = seq_sum_quad(y); sz = seq_sum_quad(z);
+        return;
+    }
     if (M <= 16) {            // walkers of M | 16 lanes sit inside one 16-lane DPP row
         a = seq_chain<0x111>(x, M); b = seq_chain<0x111>(y, M); c = seq_chain<0x111>(z, M);
     } else {
@@ -657,6 +684,7 @@ __device__ inline void seq_sum3_lanes(float x, float y, float z, int base, int M
     sx = lane_get(a, last); sy = lane_get(b, last); sz = lane_get(c, last);
 }
 __device__ inline float seq_sum_lanes(float x, int base, int M) {
+    if (M == 4) return seq_sum_quad(x);
     float a, b, c;
     seq_sum3_lanes(x, 0.f, 0.f, base, M, a, b, c);
     return a;
@@ -683,6 +711,9 @@ __device__ inline float pw_sum_lanes(float x, int base, int M, int lane) {
 }
 
 // ------------------------------------------------------------------ pair terms
+#ifndef WG_FAST_PAIR
+#define WG_FAST_PAIR 1   // 0 (A/B builds only): every pair term in its IEEE form
+#endif
 // One gravity / coulomb partner (gym/engine.py:128-147 -> anti_forced :69-76 -> forced :65-67), all float64:
 // r = max(norm(d) as float64, Config.r); f = -c*s_lo*s_hi / r**2; a = f32(f64(a) + ((-f)*d / r) / m).  The
 // divisions by r (when unclamped: a float32 value) and by m go through ddiv_f32d with one IEEE reciprocal each.
@@ -703,9 +734,6 @@ __device__ __forceinline__ void pair_central_term(double coef, double slo, doubl
     ay = (float)((double)ay + ddiv_f32d(t1, md, ym));
     az = (float)((double)az + ddiv_f32d(t2, md, ym));
 }
-#ifndef WG_FAST_PAIR
-#define WG_FAST_PAIR 1
-#endif
 // a / b by Markstein's correction from y ~ 1/b, written -(-r*y - q) so that a = +-0 gives the IEEE signed zero
 __device__ __forceinline__ double mk_div(double a, double b, double y) {
     const double q = a * y;
@@ -764,20 +792,52 @@ __device__ __forceinline__ void bounce_term(float cur, float nf, float d0, float
 // negations are exact).  cg = f32(-Config.g * m_lo * m_hi) from the Python product (numerator in float64).  A
 // distance below Config.r leaves the Python float 16e-36 in its place: f and the division then go through its
 // float32 casts (:189-192 with a Python-float distance).
-__device__ __forceinline__ void g2_gravity_term(double cgd, float d0, float d1, float d2, float mf, float &ax,
-                                                float &ay, float &az) {
+// The reference arithmetic of one partner (IEEE float32 divisions and sqrtf): the three quotients force_c / m.
+__device__ __forceinline__ void g2_gravity_cold(double cgd, float d0, float d1, float d2, float mf, float &q0, float &q1,
+                                             float &q2) {
     const float dist = np_norm3(d0, d1, d2);
     float f, dv;
-    if (__builtin_expect(!(CONFIG_R > (double)dist), 1)) {   // unclamped (NaN too: max keeps the float32 NaN)
-        f = (float)cgd / np_sq(dist);
+    if (!(CONFIG_R > (double)dist)) {        // unclamped (NaN too: max keeps the float32 NaN)
+        f = (float)cgd / pw_pow2(dist);
         dv = dist;
     } else {
-        f = (float)(cgd / (CONFIG_R * CONFIG_R));              // Python floats throughout, cast where they meet float32
+        f = (float)(cgd / (CONFIG_R * CONFIG_R));   // Python floats throughout, cast where they meet float32
         dv = (float)CONFIG_R;
     }
-    ax = ax + ((f * d0) / dv) / mf;
-    ay = ay + ((f * d1) / dv) / mf;
-    az = az + ((f * d2) / dv) / mf;
+    q0 = ((f * d0) / dv) / mf;
+    q1 = ((f * d1) / dv) / mf;
+    q2 = ((f * d2) / dv) / mf;
+}
+// RN32(a / b) for a float32 a and b from y ~ 1/b (rcp64_nr, within ~1 ulp of a double): the double product a * y lies
+// within 2^-51 (relative) of a / b, and a quotient of two 24-bit floats is at least 2^-47 from every float32 rounding
+// midpoint (subnormal results included), so the one rounding to float32 is RN32(a / b); zero, inf and NaN
+// numerators propagate as IEEE division does.  b must be finite, nonzero and normal (the callers' guards).
+__device__ __forceinline__ float fdiv_rcp(float a, double y) { return (float)((double)a * y); }
+// G2 gravity_vec partner, fast form: np_norm3's sum, sqrt_mid, numpy's distance ** 2 by pw_pow2_fast, the four
+// quotients by fdiv_rcp from two reciprocals, the division by m from ym = RN64(1/m) (fdiv_exact).  ok = false when a
+// guard fails (the squared distance outside [2^-96, 2^126): sqrt_mid's range, which also keeps the distance clear of
+// Config.r; the powf fast path undecided); the caller then takes g2_gravity_cold for this partner.
+__device__ __forceinline__ void g2_gravity_fast(float cg, float d0, float d1, float d2, double ym, float &q0,
+                                                float &q1, float &q2, bool &ok) {
+    const float sq = (float)(((double)(d0 * d0) + (double)(d1 * d1)) + (double)(d2 * d2));
+    const float dist = sqrt_mid(sq);
+    float dd;
+    ok = pw_pow2_fast(dist, &dd) && sq >= 0x1p-96f && sq < 0x1p126f;
+    const float f = fdiv_rcp(cg, rcp64_nr((double)dd));
+    const double yd = rcp64_nr((double)dist);
+    q0 = fdiv_exact(fdiv_rcp(f * d0, yd), ym);
+    q1 = fdiv_exact(fdiv_rcp(f * d1, yd), ym);
+    q2 = fdiv_exact(fdiv_rcp(f * d2, yd), ym);
+}
+__device__ __forceinline__ void g2_gravity_term(double cgd, float d0, float d1, float d2, float mf, double ym,
+                                                float &ax, float &ay, float &az) {
+    float q0, q1, q2;
+    bool ok = WG_FAST_PAIR;
+    if (WG_FAST_PAIR) g2_gravity_fast((float)cgd, d0, d1, d2, ym, q0, q1, q2, ok);
+    if (__builtin_expect(!ok, 0)) g2_gravity_cold(cgd, d0, d1, d2, mf, q0, q1, q2);
+    ax = ax + q0;
+    ay = ay + q1;
+    az = az + q2;
 }
 
 // ------------------------------------------------------------------ pair passes from LDS (workgroup kernel)
@@ -876,7 +936,7 @@ __device__ void pair_forces_lds(const wg_batch &b, const KParams &kp, const floa
             const float *o3 = spos + 3 * (lm + pj);
             const double mo = (double)sm[lm + pj];
             g2_gravity_term(((-kp.pair_g) * (pj < q ? mo : md)) * (pj < q ? md : mo), o3[0] - p3[0], o3[1] - p3[1],
-                            o3[2] - p3[2], mf, ax, ay, az);
+                            o3[2] - p3[2], mf, ym, ax, ay, az);
         }
     }
     if (kp.pair_mode & 16)                   // Point.electrostatic (gym/engine.py:150-158) of every point
@@ -1571,7 +1631,7 @@ __device__ __forceinline__ void pair_bounce(float kh, double rs, const float *p3
 __device__ __forceinline__ void pair_g2_gravity(double g, const float *p3, float mf, int lane, int M, bool is_mass,
                                                 float &ax, float &ay, float &az) {
     const int gb = lane & ~(M - 1), q = lane & (M - 1);
-    const double md = (double)mf;
+    const double md = (double)mf, ym = 1.0 / md;
     ax = 0.f; ay = 0.f; az = 0.f;
     for (int pj = 0; pj < M; pj++) {
         const int src = (gb + pj) << 2;
@@ -1579,8 +1639,8 @@ __device__ __forceinline__ void pair_g2_gravity(double g, const float *p3, float
         const float om = lane_gather(mf, src);
         if (!is_mass || pj == q) continue;
         const double mo = (double)om;
-        g2_gravity_term(((-g) * (pj < q ? mo : md)) * (pj < q ? md : mo), ox - p3[0], oy - p3[1], oz - p3[2], mf, ax,
-                        ay, az);
+        g2_gravity_term(((-g) * (pj < q ? mo : md)) * (pj < q ? md : mo), ox - p3[0], oy - p3[1], oz - p3[2], mf, ym,
+                        ax, ay, az);
     }
 }
 
@@ -1825,7 +1885,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lean_waves(
     LeanGeo lg) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int tile = blockIdx.x * lg.wpb + wv;
+    const int blk = (kp.xcd & 2) ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int tile = blk * lg.wpb + wv;
     if (tile * lg.wpw >= b.N) return;
 #ifdef WG_STAMPS
     const int stamp_wave = tile;
@@ -1927,7 +1988,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
     // the wave index as a wave-uniform (scalar) value: the plan entries and the tile's bases are then scalar loads
     // (scalar cache, lgkmcnt) rather than vector loads each waited for before the next one can be addressed
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int tile = blockIdx.x * rg.wpb + wv;
+    const int blk = (kp.xcd & 1) ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int tile = blk * rg.wpb + wv;
     if (tile >= ntiles) return;
 #ifdef WG_STAMPS
     const int stamp_wave = tile;
@@ -2251,6 +2313,7 @@ KParams make_kparams(const wg_params &p) {
     k.g3_ground = p.g3_ground;
     k.friction_mode = p.friction_mode;
     k.prio = env_int("WG_LEAN_PRIO", 1);
+    k.xcd = env_int("WG_XCD", 1);
     k.dt2 = (float)(p.dt * p.dt);
     return k;
 }

@@ -176,7 +176,8 @@ class BatchedPhysicsEnv:
         N, D, dv = self.N, self.obs_dim, self.device
         self.obs = torch.zeros((N, D), dtype=torch.float32, device=dv)
         self.reward = torch.zeros(N, dtype=torch.float32, device=dv)
-        self.done = torch.zeros(N, dtype=torch.uint8, device=dv)
+        # bool storage: the kernel writes 0 / 1 bytes, so step() returns it as is (no conversion launch per step)
+        self.done = torch.zeros(N, dtype=torch.bool, device=dv)
         self.centroid = torch.zeros((N, 3), dtype=torch.float32, device=dv)
         self.energy = torch.zeros(N, dtype=torch.float32, device=dv)
 
@@ -245,14 +246,14 @@ class BatchedPhysicsEnv:
             self._run_lanes(act[None], 1, lambda w0, w1: self._outputs(
                 self.obs[w0:w1], self.reward[w0:w1], self.done[w0:w1], self.centroid[w0:w1], self.energy[w0:w1],
                 pad_clean=True), lanes)
-            return self.obs, self.reward, self.done.bool(), self.info()
+            return self.obs, self.reward, self.done, self.info()
         L = _lib.load()
         o = self._outputs(self.obs, self.reward, self.done, self.centroid, self.energy, pad_clean=True)
         _lib.check(L.wg_step(C.byref(self.batch.struct), C.byref(self._pstruct),
                              None if act is None else C.c_void_p(act.data_ptr()), cols, cols, 0, C.byref(o), 1,
                              None if self.batch.plan is None else C.c_void_p(self.batch.plan.data_ptr()),
                              self.batch.plan_blocks, self._stream()), "wg_step")
-        return self.obs, self.reward, self.done.bool(), self.info()
+        return self.obs, self.reward, self.done, self.info()
 
     def rollout(self, actions, obs_out=None, reward_out=None, done_out=None, lanes: Optional[int] = None,
                 resident: bool = True):
@@ -405,7 +406,7 @@ class BatchedPhysicsEnv:
             C.byref(self.batch.struct), C.byref(self._pstruct), C.byref(o),
             None if self.batch.plan is None else C.c_void_p(self.batch.plan.data_ptr()),
             self.batch.plan_blocks, self._stream()), "wg_observe")
-        return self.obs, self.reward, self.done.bool(), self.info()
+        return self.obs, self.reward, self.done, self.info()
 
     def reset(self, noise=None, mask=None):
         """PhysicsEnv.reset: v += N(0, sigma) noise on x, y (and z if in3d); steps = 0; returns obs.

@@ -53,6 +53,8 @@ int main(void) {
   F(wg_batch, pos) F(wg_batch, edges) F(wg_batch, inc_off) F(wg_batch, muscle_bounds) F(wg_batch, contact)
   F(wg_outputs, obs_step) F(wg_outputs, out_step) F(wg_params, in3d) F(wg_params, action_mode) F(wg_params, pair_g)
   F(wg_params, bounce_k) F(wg_batch, charge) F(wg_batch, radius)
+  printf("wg_range %zu\\n", sizeof(wg_range));
+  F(wg_range, outputs) F(wg_range, action_offset) F(wg_range, plan) F(wg_range, plan_blocks) F(wg_range, stream)
   return 0;
 }
 """)
@@ -65,7 +67,9 @@ int main(void) {
     assert int(got["wg_outputs"]) == C.sizeof(_lib.WgOutputs)
     assert int(got["wg_launch_info"]) == C.sizeof(_lib.WgLaunchInfo)
     assert int(got["wg_edge"]) == 16
-    for key, cls in (("wg_batch", _lib.WgBatch), ("wg_outputs", _lib.WgOutputs), ("wg_params", _lib.WgParams)):
+    assert int(got["wg_range"]) == C.sizeof(_lib.WgRange)
+    for key, cls in (("wg_batch", _lib.WgBatch), ("wg_outputs", _lib.WgOutputs), ("wg_params", _lib.WgParams),
+                     ("wg_range", _lib.WgRange)):
         for full, off in got.items():
             if full.startswith(key + "."):
                 assert getattr(cls, full.split(".", 1)[1]).offset == int(off), full
@@ -213,3 +217,17 @@ def test_launch_geometry_small_batch_halves_tiles(lib):
     info = _lib.WgLaunchInfo()
     assert lib.wg_launch_geometry(C.byref(b), C.byref(info)) == 0
     assert info.walkers_per_block == 4 * 8 and info.blocks == 128        # 8 Balance walkers per wave, 512 tiles
+
+
+def test_step_ranges_argument_errors(lib):
+    """wg_step_ranges (ABI 8) refuses bad range lists before touching a stream: no ranges, n < 1, n > 1 without
+    events, and a range whose batch is invalid (the per-range wg_step checks)."""
+    p = _lib.WgParams()
+    assert lib.wg_step_ranges(None, 1, C.byref(p), None, 0, 0, None) == _lib.WG_EINVAL
+    rng = (_lib.WgRange * 2)()
+    assert lib.wg_step_ranges(rng, 0, C.byref(p), None, 0, 0, None) == _lib.WG_EINVAL
+    assert lib.wg_step_ranges(rng, 2, C.byref(p), None, 0, 0, None) == _lib.WG_EINVAL
+    assert b"events" in lib.wg_last_error()
+    bad = _lib.WgBatch(N=4, M=0, K=1, A=0)
+    rng[0].batch = C.pointer(bad)
+    assert lib.wg_step_ranges(rng, 1, C.byref(p), None, 0, 0, None) == _lib.WG_EINVAL

@@ -13,7 +13,7 @@ import threading
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libwalker_hip.so"
 LIB_PATH = os.path.join(HERE, LIB_NAME)
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 WG_EINVAL, WG_ERANGE, WG_EHIP = -1, -2, -3
 
@@ -49,12 +49,17 @@ class WgOutputs(C.Structure):
                 ("obs_pad_clean", C.c_int32)]
 
 
+class WgRange(C.Structure):
+    _fields_ = [("batch", C.POINTER(WgBatch)), ("outputs", C.POINTER(WgOutputs)), ("action_offset", C.c_int64),
+                ("plan", _vp), ("plan_blocks", C.c_int32), ("stream", _vp)]
+
+
 class WgLaunchInfo(C.Structure):
     _fields_ = [("threads", C.c_int32), ("walkers_per_block", C.c_int32), ("blocks", C.c_int32),
                 ("lds_bytes", C.c_int32)]
 
 
-EXPORTS = ("wg_abi_version", "wg_last_error", "wg_step", "wg_rollout", "wg_observe", "wg_reset", "wg_reset_noise",
+EXPORTS = ("wg_abi_version", "wg_last_error", "wg_step", "wg_step_ranges", "wg_rollout", "wg_observe", "wg_reset", "wg_reset_noise",
            "wg_plan_ragged", "wg_plan_waves", "wg_wave_edge_passes", "wg_launch_geometry")
 
 _lib = None
@@ -82,6 +87,8 @@ def load(path: str | None = None):
         L.wg_step.argtypes = [C.POINTER(WgBatch), C.POINTER(WgParams), _vp, C.c_int32, C.c_int32, C.c_int64,
                               C.POINTER(WgOutputs), C.c_int32, _vp, C.c_int32, _vp]
         L.wg_rollout.argtypes = L.wg_step.argtypes
+        L.wg_step_ranges.argtypes = [C.POINTER(WgRange), C.c_int32, C.POINTER(WgParams), _vp, C.c_int32, C.c_int32,
+                                     C.POINTER(_vp)]
         L.wg_observe.argtypes = [C.POINTER(WgBatch), C.POINTER(WgParams), C.POINTER(WgOutputs), _vp, C.c_int32, _vp]
         L.wg_reset.argtypes = [C.POINTER(WgBatch), C.POINTER(WgParams), _vp, _vp, _vp]
         L.wg_reset_noise.argtypes = [C.POINTER(WgBatch), _vp, _vp]
@@ -89,7 +96,7 @@ def load(path: str | None = None):
         L.wg_plan_waves.argtypes = [_vp, _vp, _vp, C.c_int32, _vp, C.c_int32]
         L.wg_wave_edge_passes.argtypes = [C.c_int32, C.c_int32]
         L.wg_launch_geometry.argtypes = [C.POINTER(WgBatch), C.POINTER(WgLaunchInfo)]
-        for f in ("wg_step", "wg_rollout", "wg_observe", "wg_reset", "wg_reset_noise", "wg_plan_ragged", "wg_plan_waves",
+        for f in ("wg_step", "wg_step_ranges", "wg_rollout", "wg_observe", "wg_reset", "wg_reset_noise", "wg_plan_ragged", "wg_plan_waves",
                   "wg_wave_edge_passes", "wg_launch_geometry"):
             getattr(L, f).restype = C.c_int
         v = L.wg_abi_version()

@@ -227,6 +227,9 @@ class BatchedPhysicsEnv:
     def _check_action(self, action):
         if action is None:
             return None, 0
+        if (isinstance(action, torch.Tensor) and action.dim() == 2 and action.dtype == torch.float32
+                and action.device == self.device and action.shape[0] == self.N and action.is_contiguous()):
+            return action, action.shape[1]                      # the closed-loop fast path: used as given
         if not isinstance(action, torch.Tensor):
             action = torch.as_tensor(np.asarray(action, dtype=np.float32))
         action = action.to(self.device, torch.float32)
@@ -239,21 +242,69 @@ class BatchedPhysicsEnv:
     # ------------------------------------------------------------------ API
     def step(self, action=None):
         """One env step for all walkers: act -> physics -> run1 -> obs/reward/done/info: one launch per walker range
-        (the default ranges, joined on the calling stream before this returns its outputs)."""
+        (the default ranges, forked from and joined back to the calling stream inside one wg_step_ranges call).  The
+        C arguments of every range are built once and cached (_step_plan): a closed-loop caller pays one ctypes
+        call per step."""
         act, cols = self._check_action(action)
-        lanes = self._lanes(None)
-        if act is not None and lanes > 1:
-            self._run_lanes(act[None], 1, lambda w0, w1: self._outputs(
-                self.obs[w0:w1], self.reward[w0:w1], self.done[w0:w1], self.centroid[w0:w1], self.energy[w0:w1],
-                pad_clean=True), lanes)
-            return self.obs, self.reward, self.done, self.info()
-        L = _lib.load()
-        o = self._outputs(self.obs, self.reward, self.done, self.centroid, self.energy, pad_clean=True)
-        _lib.check(L.wg_step(C.byref(self.batch.struct), C.byref(self._pstruct),
-                             None if act is None else C.c_void_p(act.data_ptr()), cols, cols, 0, C.byref(o), 1,
-                             None if self.batch.plan is None else C.c_void_p(self.batch.plan.data_ptr()),
-                             self.batch.plan_blocks, self._stream()), "wg_step")
+        plan = self._step_plan(cols if act is not None else -1)
+        cur = torch.cuda.current_stream(self.device)
+        rng = plan["ranges"]
+        rng[0].stream = cur.cuda_stream
+        rc = plan["fn"](rng, plan["n"], self._pref, act.data_ptr() if act is not None else None, cols, cols,
+                        plan["events"])
+        if rc:
+            _lib.check(rc, "wg_step_ranges")
+        if act is not None and plan["n"] > 1:
+            for st in plan["side"]:
+                act.record_stream(st)   # the allocator must not recycle the actions before the side streams read them
         return self.obs, self.reward, self.done, self.info()
+
+    def _step_plan(self, cols: int) -> dict:
+        """step()'s wg_step_ranges arguments for this env's own output tensors, cached per (generation, batch struct,
+        action columns): one wg_range per walker range (uniform: offset batch views; ragged: plan slices), the
+        outputs, the action element offset of each range, its stream, and the fork / join events."""
+        key = (self._generation, id(self.batch.struct), cols)
+        cached = getattr(self, "_plan_cache", None)
+        if cached is not None and cached["key"] == key:
+            return cached
+        lanes = self._lanes(None) if cols >= 0 else 1
+        self.reserve_streams(lanes)
+        b = self.batch
+        keep = []                                  # the ctypes structs the ranges point at
+        rng = (_lib.WgRange * lanes)()
+
+        def out(w0, w1):
+            o = self._outputs(self.obs[w0:w1], self.reward[w0:w1], self.done[w0:w1], self.centroid[w0:w1],
+                              self.energy[w0:w1], pad_clean=True)
+            keep.append(o)
+            return C.pointer(o)
+        if lanes == 1 or b.ragged:
+            nb = b.plan_blocks
+            bounds = [nb * i // lanes for i in range(lanes)] + [nb]
+            o = out(0, self.N)
+            for i in range(lanes):
+                rng[i].batch, rng[i].outputs, rng[i].action_offset = C.pointer(b.struct), o, 0
+                rng[i].plan = None if b.plan is None else b.plan.data_ptr() + 4 * bounds[i]
+                rng[i].plan_blocks = bounds[i + 1] - bounds[i] if b.plan is not None else 0
+        else:
+            bounds = [0] + [((self.N * i // lanes) + 63) // 64 * 64 for i in range(1, lanes)] + [self.N]
+            for i in range(lanes):
+                w0, w1 = bounds[i], bounds[i + 1]
+                sub = b.sub_struct(w0, w1)
+                keep.append(sub)
+                rng[i].batch, rng[i].outputs = C.pointer(sub), out(w0, w1)
+                rng[i].action_offset, rng[i].plan, rng[i].plan_blocks = w0 * max(cols, 0), None, 0
+        side = self._side[:lanes - 1]
+        for i, st in enumerate(side):
+            rng[i + 1].stream = st.cuda_stream
+        events = [torch.cuda.Event() for _ in range(lanes)]
+        for ev in events:
+            ev.record()                            # materialise the hipEvent handle
+        self._pref = C.byref(self._pstruct)
+        self._plan_cache = {"key": key, "fn": _lib.load().wg_step_ranges, "ranges": rng, "n": lanes, "side": side,
+                            "keep": keep, "events_obj": events,
+                            "events": (C.c_void_p * lanes)(*[ev.cuda_event for ev in events])}
+        return self._plan_cache
 
     def rollout(self, actions, obs_out=None, reward_out=None, done_out=None, lanes: Optional[int] = None,
                 resident: bool = True):

@@ -813,16 +813,17 @@ __device__ __forceinline__ void g2_gravity_cold(double cgd, float d0, float d1, 
 // midpoint (subnormal results included), so the one rounding to float32 is RN32(a / b); zero, inf and NaN
 // numerators propagate as IEEE division does.  b must be finite, nonzero and normal (the callers' guards).
 __device__ __forceinline__ float fdiv_rcp(float a, double y) { return (float)((double)a * y); }
-// G2 gravity_vec partner, fast form: np_norm3's sum, sqrt_mid, numpy's distance ** 2 by pw_pow2_fast, the four
-// quotients by fdiv_rcp from two reciprocals, the division by m from ym = RN64(1/m) (fdiv_exact).  ok = false when a
-// guard fails (the squared distance outside [2^-96, 2^126): sqrt_mid's range, which also keeps the distance clear of
-// Config.r; the powf fast path undecided); the caller then takes g2_gravity_cold for this partner.
+// G2 gravity_vec partner, fast form: np_norm3's sum, sqrt_mid, numpy's distance ** 2 (np_sq: RN(x*x) or, for the
+// 0.29 % of distances near a rounding boundary, the restated powf), the four quotients by fdiv_rcp from two
+// reciprocals, the division by m from ym = RN64(1/m) (fdiv_exact).  ok = false when the squared distance leaves
+// [2^-96, 2^126) (sqrt_mid's range, which also keeps the distance clear of Config.r); the caller then takes
+// g2_gravity_cold for this partner.
 __device__ __forceinline__ void g2_gravity_fast(float cg, float d0, float d1, float d2, double ym, float &q0,
                                                 float &q1, float &q2, bool &ok) {
     const float sq = (float)(((double)(d0 * d0) + (double)(d1 * d1)) + (double)(d2 * d2));
     const float dist = sqrt_mid(sq);
-    float dd;
-    ok = pw_pow2_fast(dist, &dd) && sq >= 0x1p-96f && sq < 0x1p126f;
+    ok = sq >= 0x1p-96f && sq < 0x1p126f;
+    const float dd = np_sq(dist);
     const float f = fdiv_rcp(cg, rcp64_nr((double)dd));
     const double yd = rcp64_nr((double)dist);
     q0 = fdiv_exact(fdiv_rcp(f * d0, yd), ym);
@@ -1499,10 +1500,32 @@ __device__ __forceinline__ LeanTile lean_tile_of(const wg_batch &b, const float 
 // words, mass-loop inputs, muscles.  (Issuing what the springs need first and the mass-loop inputs last measured
 // 48.5 against 47.7 us per launch, profiles/r02_ab_loadorder_karg.json: in steady state a wave spends ~4K of its
 // ~25K cycles on loads, so there is little latency left to hide.)
+#ifndef WG_LEAN_CLAMP
+#define WG_LEAN_CLAMP 1
+#endif
+// A global array element at a 32-bit byte offset from a kernel-argument base: the address is SGPR base + zero-extended
+// VGPR offset, which the global_load's saddr form takes as is (no 64-bit address arithmetic per load).
+template <typename T>
+__device__ __forceinline__ const T &at_u32(const T *base, uint32_t byte_off) {
+    // (WG_LEAN_CLAMP=0, A/B builds only: a sign-extended offset, which keeps the 64-bit VALU address arithmetic)
+    const size_t off = WG_LEAN_CLAMP ? (size_t)byte_off : (size_t)(int64_t)(int32_t)byte_off;
+    return *reinterpret_cast<const T *>(reinterpret_cast<const char *>(base) + off);
+}
 template <int NE>
 __device__ __forceinline__ void lean_load_mass(const wg_batch &b, const LeanTile &t, int lane, LeanIn<NE> &L) {
-    const uint32_t pl = t.P0 + lane;
     L.mf = 0.f; L.io0 = 0; L.io1 = 0; L.wsteps = 0; L.pin = 0;
+    if (WG_LEAN_CLAMP) {
+        // every lane loads (lanes past the tile's masses a duplicate of its last one; their values are never used)
+        const int ln = min(lane, t.nP - 1);
+        const int wl = ln >> (31 - __builtin_clz(b.M)), q = ln & (b.M - 1);
+        L.mf = at_u32(b.mass, 4u * (t.P0 + ln));
+        if (b.pinned) L.pin = at_u32(b.pinned, t.P0 + ln);
+        const uint32_t io = (uint32_t)(t.w0 + wl) * (b.M + 1) + q;
+        L.io0 = at_u32(b.inc_off, 2u * io); L.io1 = at_u32(b.inc_off, 2u * io + 2u);
+        L.wsteps = at_u32(b.steps, 4u * (uint32_t)(t.w0 + wl));   // the walker's counter in each of its lanes
+        return;
+    }
+    const uint32_t pl = t.P0 + lane;
     if (t.is_mass) {
         L.mf = b.mass[pl];
         if (b.pinned) L.pin = b.pinned[pl];
@@ -1515,6 +1538,20 @@ template <int NE>
 __device__ __forceinline__ void lean_load_muscles(const wg_batch &b, const KParams &kp, const float *__restrict__ action,
                                                   int action_stride, const LeanTile &t, int lane, LeanIn<NE> &L) {
     L.x = 0.f; L.lo = 0.f; L.hi = 0.f; L.stp = 0.f; L.a = 0.f;
+    if (WG_LEAN_CLAMP) {
+        if (t.nU > 0) {                       // wave-uniform
+            const uint32_t ul = t.U0 + min(lane, t.nU - 1);
+            L.x = at_u32(b.muscle_x, 4u * ul);
+            if (action && action_stride > 0) {
+                const float2 bd = at_u32(reinterpret_cast<const float2 *>(b.muscle_bounds), 8u * ul);
+                L.lo = bd.x; L.hi = bd.y;
+                if (kp.action_mode == 1) L.stp = at_u32(b.muscle_stride, 4u * ul);
+                const int wl = min(t.mu_wl, t.nw - 1), ua = max(0, min(t.mu_ua, action_stride - 1));
+                L.a = at_u32(action, 4u * ((uint32_t)(t.w0 + wl) * (uint32_t)action_stride + (uint32_t)ua));
+            }
+        }
+        return;
+    }
     const uint32_t ul = t.U0 + lane;        // this lane's muscle
     if (t.is_mus) {
         L.x = b.muscle_x[ul];
@@ -1529,6 +1566,31 @@ __device__ __forceinline__ void lean_load_muscles(const wg_batch &b, const KPara
 template <int NE>
 __device__ __forceinline__ void lean_load(const wg_batch &b, const KParams &kp, const float *__restrict__ action,
                                           int action_stride, const LeanTile &t, int lane, LeanIn<NE> &L) {
+    if (WG_LEAN_CLAMP) {
+        // every load unconditional from a clamped (valid) index, issued back to back: no exec-mask branch per load
+        // (each with its zero-fill moves), addresses as SGPR base + 32-bit offset.  Lanes past the tile's masses,
+        // springs and muscles hold duplicates; every use of them is gated (is_mass, le < nE, is_mus, acts).
+        const uint32_t pl = t.P0 + min(lane, t.nP - 1);
+        const float *gp = &at_u32(b.pos, 12u * pl), *gv = &at_u32(b.vel, 12u * pl);
+        L.p3[0] = gp[0]; L.p3[1] = gp[1]; L.p3[2] = gp[2];
+        L.v3[0] = gv[0]; L.v3[1] = gv[1]; L.v3[2] = gv[2];
+#pragma unroll
+        for (int it = 0; it < NE; it++) {
+            const uint32_t le = t.E0 + (uint32_t)min(lane + 64 * it, t.nE - 1);
+            const uint4 v = at_u32(reinterpret_cast<const uint4 *>(b.edges), 16u * le);
+            L.er[it] = EdgeRec{v.x, __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w)};
+            L.gi[it] = at_u32(reinterpret_cast<const uint32_t *>(b.inc), 4u * le);
+        }
+        lean_load_mass<NE>(b, t, lane, L);
+        lean_load_muscles<NE>(b, kp, action, action_stride, t, lane, L);
+        if (!t.is_mass) {                     // the reference values of the lanes past the tile's masses
+            L.p3[0] = 0.f; L.p3[1] = 0.f; L.p3[2] = 0.f; L.v3[0] = 0.f; L.v3[1] = 0.f; L.v3[2] = 0.f;
+            L.mf = 0.f; L.pin = 0; L.io0 = 0; L.io1 = 0;
+        }
+        if (!t.is_mus) { L.x = 0.f; L.lo = 0.f; L.hi = 0.f; L.stp = 0.f; }
+        if (!t.acts) L.a = 0.f;
+        return;
+    }
     const uint32_t pl = t.P0 + lane;        // this lane's mass
     L.p3[0] = 0.f; L.p3[1] = 0.f; L.p3[2] = 0.f;
     L.v3[0] = 0.f; L.v3[1] = 0.f; L.v3[2] = 0.f;
@@ -2018,40 +2080,42 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
     // load a duplicate and are given the reference values (zeros) once everything has landed.
     const bool is_mass = lane < nP, is_mus = lane < nU;
     const int lw = min(lane, nw), lr = min(lane, nw - 1);
-    int wmo = b.mass_off[w0 + lw] - P0, weo = b.edge_off[w0 + lw] - E0, wuo = b.muscle_off[w0 + lw] - U0;
-    int wsteps = b.steps[w0 + lr];
+    // (addresses as SGPR base + 32-bit byte offset: the saddr form of global_load, no 64-bit VALU arithmetic)
+    int wmo = at_u32(b.mass_off, 4u * (w0 + lw)) - P0, weo = at_u32(b.edge_off, 4u * (w0 + lw)) - E0;
+    int wuo = at_u32(b.muscle_off, 4u * (w0 + lw)) - U0;
+    int wsteps = at_u32(b.steps, 4u * (w0 + lr));
     const int lp = P0 + min(lane, max(nP, 1) - 1);   // a tile has at least one mass
     float p3[3], v3[3];
     {
-        const float *gp = b.pos + 3 * (size_t)lp, *gv = b.vel + 3 * (size_t)lp;
+        const float *gp = &at_u32(b.pos, 12u * lp), *gv = &at_u32(b.vel, 12u * lp);
         p3[0] = gp[0]; p3[1] = gp[1]; p3[2] = gp[2];
         v3[0] = gv[0]; v3[1] = gv[1]; v3[2] = gv[2];
     }
-    float mf = b.mass[lp];
+    float mf = at_u32(b.mass, 4u * lp);
     EdgeRec er[NE];
     uint32_t gi[NE];
     if (nE > 0) {
-        const uint32_t *incw = reinterpret_cast<const uint32_t *>(b.inc) + E0;
 #pragma unroll
         for (int it = 0; it < NE; it++) {
-            const int le = min(lane + 64 * it, nE - 1);
-            er[it] = load_edge(b.edges, E0 + le);
-            gi[it] = incw[le];
+            const uint32_t le = E0 + min(lane + 64 * it, nE - 1);
+            const uint4 v = at_u32(reinterpret_cast<const uint4 *>(b.edges), 16u * le);
+            er[it] = EdgeRec{v.x, __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w)};
+            gi[it] = at_u32(reinterpret_cast<const uint32_t *>(b.inc), 4u * le);
         }
     }
     float mx = 0.f, mlo = 0.f, mhi = 0.f, mst = 0.f;
     if (nU > 0) {
-        const int lu = U0 + min(lane, nU - 1);
-        mx = b.muscle_x[lu];
+        const uint32_t lu = U0 + min(lane, nU - 1);
+        mx = at_u32(b.muscle_x, 4u * lu);
         if (action) {
-            const float2 bd = reinterpret_cast<const float2 *>(b.muscle_bounds)[lu];
+            const float2 bd = at_u32(reinterpret_cast<const float2 *>(b.muscle_bounds), 8u * lu);
             mlo = bd.x; mhi = bd.y;
-            if (kp.action_mode == 1) mst = b.muscle_stride[lu];
+            if (kp.action_mode == 1) mst = at_u32(b.muscle_stride, 4u * lu);
         }
     }
     int wrow = w0 + lr, pin = 0;
-    if (b.row) wrow = b.row[w0 + lr];
-    if (b.pinned) pin = b.pinned[lp];
+    if (b.row) wrow = at_u32(b.row, 4u * (w0 + lr));
+    if (b.pinned) pin = at_u32(b.pinned, (uint32_t)lp);
     // lane -> walker maps (tile-local offsets in LDS)
     if (lane <= nw) { s_mo[lane] = wmo; s_eo[lane] = weo; s_uo[lane] = wuo; }
     if (lane < nw) s_row[lane] = wrow;
@@ -2074,12 +2138,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
     const int mlm = s_mo[mw], mM = s_mo[mw + 1] - mlm, mlb = s_eo[mw];
     // inc_off (M_w + 1 entries per walker) and the action: the second (and last) round of vector loads
     const uint32_t io = (uint32_t)lp + (uint32_t)(w0 + mw);
-    int io0 = b.inc_off[io], io1 = b.inc_off[io + 1];
+    int io0 = at_u32(b.inc_off, 2u * io), io1 = at_u32(b.inc_off, 2u * io + 2u);
     const int ua = lane - s_uo[uw];                                      // this lane's muscle in walker uw
     const bool acts = action != nullptr && is_mus && ua < action_cols;
     float act = 0.f;
     if (action && action_cols > 0)
-        act = action[(size_t)s_row[uw] * action_stride + min(max(ua, 0), action_cols - 1)];
+        act = at_u32(action, 4u * ((uint32_t)s_row[uw] * (uint32_t)action_stride + (uint32_t)min(max(ua, 0), action_cols - 1)));
     // the reference values of the lanes past the tile's masses / muscles (the loads above read duplicates)
     if (!is_mass) {
         p3[0] = 0.f; p3[1] = 0.f; p3[2] = 0.f; v3[0] = 0.f; v3[1] = 0.f; v3[2] = 0.f;
@@ -2313,7 +2377,7 @@ KParams make_kparams(const wg_params &p) {
     k.g3_ground = p.g3_ground;
     k.friction_mode = p.friction_mode;
     k.prio = env_int("WG_LEAN_PRIO", 1);
-    k.xcd = env_int("WG_XCD", 1);
+    k.xcd = env_int("WG_XCD", 3);   // both kernels (profiles/r03e_ab_canon.json, r03d_ab_ragged_window_xcd.json)
     k.dt2 = (float)(p.dt * p.dt);
     return k;
 }
@@ -2428,13 +2492,21 @@ int env_int(const char *name, int dflt) {
 
 bool lean_enabled() { return env_int("WG_LEAN", 1) != 0; }
 
+// The barrier-free kernels address their loads as SGPR base + 32-bit byte offset (at_u32): every array of the batch
+// must then span less than 4 GiB (positions 12 B and spring records 16 B per element dominate; M, K are maxima).
+bool u32_bytes(const wg_batch *b) {
+    const int64_t lim = 1ll << 32;
+    return (int64_t)b->N * b->M * 12 < lim && (int64_t)b->N * b->K * 16 < lim && (int64_t)b->N * b->A * 8 < lim &&
+           (int64_t)b->N * (b->M + 1) * 2 < lim;
+}
+
 bool lean_geo(const wg_batch *b, int obs_stride, LeanGeo *out, int spring_mode = 0) {
     const int M = b->M;
     if (b->ragged || M < 4 || M > 64 || (64 % M) != 0 || b->K < 1 || !lean_enabled() || (WG_ABLATE & 128)) return false;
     if (spring_mode != 0) return false;          // the G2-compat element runs on the workgroup kernel
-    // 32-bit element offsets inside the kernel
+    // 32-bit element offsets inside the kernel, 32-bit byte offsets for its loads (at_u32)
     if ((int64_t)b->N * b->M * 3 >= (1ll << 31) || (int64_t)b->N * b->K * 4 >= (1ll << 31) ||
-        (int64_t)b->N * std::max(obs_stride, 1) >= (1ll << 31))
+        (int64_t)b->N * std::max(obs_stride, 1) >= (1ll << 31) || !u32_bytes(b))
         return false;
     LeanGeo g{};
     g.wpw = 64 / M;
@@ -2529,7 +2601,7 @@ int wave_passes(int M, int K) {
 
 bool rag_geo(const wg_batch *b, int obs_stride, RagGeo *out) {
     const int ne = wave_passes(b->M, b->K);
-    if (b->ragged != 2 || ne == 0 || b->A > 64) return false;
+    if (b->ragged != 2 || ne == 0 || b->A > 64 || !u32_bytes(b)) return false;
     RagGeo g{};
     const int wpb = env_int("WG_LEAN_WAVES", 4);
     g.wpb = (wpb == 1 || wpb == 2) ? wpb : 4;
@@ -2608,9 +2680,10 @@ int run(const wg_batch *b, const wg_params *p, const float *action, int32_t cols
     if (g.W > g.threads) return fail(WG_ERANGE, "more than %d walkers per workgroup", g.threads);
     const int blocks = b->ragged ? plan_blocks : (b->N + g.W - 1) / g.W;
     LeanGeo lg{};
-    const bool use_lean = step && lean_geo(b, out.obs ? out.obs_stride : 0, &lg, p->spring_mode);
+    const bool act_u32 = !action || (int64_t)b->N * astride * 4 < (1ll << 32);   // at_u32 action offsets
+    const bool use_lean = step && act_u32 && lean_geo(b, out.obs ? out.obs_stride : 0, &lg, p->spring_mode);
     RagGeo rgeo{};
-    const bool use_waves = step && p->spring_mode == 0 && p->pair_mode == 0 && lean_enabled() &&
+    const bool use_waves = step && act_u32 && p->spring_mode == 0 && p->pair_mode == 0 && lean_enabled() &&
                            rag_geo(b, out.obs ? out.obs_stride : 0, &rgeo);
     if (p->spring_mode < 0 || p->spring_mode > 2)
         return fail(WG_EINVAL, "spring_mode %d: 0 (engine.py), 1 (G2 element), 2 (G3 engine) only", p->spring_mode);
@@ -2667,6 +2740,23 @@ int wg_rollout(const wg_batch *b, const wg_params *p, const float *action, int32
                const int32_t *plan, int32_t plan_blocks, hipStream_t stream) {
     return run(b, p, action, action_cols, action_stride, action_step, o, n_steps, plan, plan_blocks, stream, true,
                true);
+}
+
+int wg_step_ranges(const wg_range *ranges, int32_t n, const wg_params *p, const float *action, int32_t action_cols,
+                   int32_t action_stride, hipEvent_t *events) {
+    if (!ranges || n < 1 || (n > 1 && !events)) return fail(WG_EINVAL, "wg_step_ranges: bad ranges / events");
+    hipStream_t s0 = ranges[0].stream;
+    if (n > 1 && hipEventRecord(events[0], s0) != hipSuccess) return fail(WG_EHIP, "fork event record failed");
+    for (int i = 0; i < n; i++) {
+        const wg_range &r = ranges[i];
+        if (i && hipStreamWaitEvent(r.stream, events[0], 0) != hipSuccess) return fail(WG_EHIP, "fork wait failed");
+        const int rc = run(r.batch, p, action ? action + r.action_offset : nullptr, action_cols, action_stride, 0,
+                           r.outputs, 1, r.plan, r.plan_blocks, r.stream, true);
+        if (rc) return rc;
+        if (i && (hipEventRecord(events[i], r.stream) != hipSuccess || hipStreamWaitEvent(s0, events[i], 0) != hipSuccess))
+            return fail(WG_EHIP, "join event failed");
+    }
+    return 0;
 }
 
 int wg_observe(const wg_batch *b, const wg_params *p, const wg_outputs *o, const int32_t *plan,

@@ -271,3 +271,29 @@ def test_state_setters_write_through_permuted_batch():
         want = torch.rand_like(getattr(env, k))
         setattr(env, k, want)
         assert torch.equal(getattr(env, k), want), k
+
+
+def test_out_of_cap_wave_plan_is_skipped_and_reported():
+    """wg_step trusts a device plan.  A wave-tile plan whose tiles exceed the wave caps (here: every
+    walker in tile 0, empty tiles after it) must not write past the wave's LDS slice: the kernel skips such tiles
+    (their walkers keep their state) and raises the flag wg_plan_errors reads."""
+    import torch
+    from walker_gym_amd import _lib
+    from walker_gym_amd.batched_env import BatchedPhysicsEnv
+    from walker_gym_amd.synthetic import ragged_walkers
+    L = _lib.load()
+    spec = ragged_walkers(400, seed=91, mmin=4, mmax=30)
+    env = BatchedPhysicsEnv(spec, device="cuda:0", in3d=1)
+    assert env.batch.ragged_kind == 2
+    L.wg_plan_errors(1)
+    A = int(np.max(spec["n_muscles"]))
+    acts = torch.zeros((400, A), device="cuda:0")
+    env.step(acts)                                   # a valid plan: no flag
+    torch.cuda.synchronize()
+    assert L.wg_plan_errors(0) == 0
+    pos0 = env.pos.clone()
+    env.batch.plan[1:] = 400                         # tile 0 = every walker, the other tiles empty
+    env.step(acts)
+    torch.cuda.synchronize()
+    assert L.wg_plan_errors(1) == 1 and L.wg_plan_errors(0) == 0
+    assert torch.equal(env.pos, pos0)

@@ -2033,6 +2033,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
 // per-mass terms in numpy's orders (as walker_step_kernel); observation rows are assembled in LDS and streamed to
 // the caller's rows (wg_batch.row), zero padded to the stride.
 constexpr int RW_MAXW = 32;   // walkers per wave tile (planner cap)
+__device__ int g_plan_error;  // set (vector atomic) by a wave-kernel tile beyond the caps; read by wg_plan_errors
 
 struct RagGeo {
     int wpb;                  // waves per workgroup
@@ -2074,6 +2075,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
     const int w0 = plan[tile], w1 = plan[tile + 1], nw = w1 - w0;
     const int P0 = b.mass_off[w0], E0 = b.edge_off[w0], U0 = b.muscle_off[w0];
     const int nP = b.mass_off[w1] - P0, nE = b.edge_off[w1] - E0, nU = b.muscle_off[w1] - U0;
+    // a plan tile beyond the wave's caps (a caller-made plan, ADVICE r2: wg_step trusts device plans) would write past
+    // this wave's LDS slice: such a tile is skipped — its walkers keep their state — and the launch reports it through
+    // g_plan_error (wg_plan_errors); wg_plan_waves never produces one
+    if (nw < 1 || nw > RW_MAXW || nP < 1 || nP > 64 || nU > 64 || nE > 64 * NE) {
+        if (lane == 0) atomicOr(&g_plan_error, 1);
+        return;
+    }
     // every vector load that needs only the tile's bases, issued back to back from clamped (valid) indices: a load
     // under a per-lane branch whose result the register allocator copies waits right there, and with vmcnt counting
     // in order that wait covers every load before it.  Lanes past the tile's walkers / masses / springs / muscles
@@ -2776,6 +2784,18 @@ int wg_reset_noise(const wg_batch *b, const float *noise, hipStream_t stream) {
 }
 
 int wg_wave_edge_passes(int32_t M, int32_t K) { return wave_passes(M, K); }
+
+int wg_plan_errors(int32_t clear) {
+    int v = 0;
+    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_plan_error), sizeof v, 0, hipMemcpyDeviceToHost) != hipSuccess)
+        return fail(WG_EHIP, "plan error flag copy failed");
+    if (clear && v) {
+        const int z = 0;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_plan_error), &z, sizeof z, 0, hipMemcpyHostToDevice) != hipSuccess)
+            return fail(WG_EHIP, "plan error flag reset failed");
+    }
+    return v;
+}
 
 int wg_plan_waves(const int32_t *mass_off, const int32_t *edge_off, const int32_t *muscle_off, int32_t N,
                   int32_t *plan, int32_t max_tiles) {

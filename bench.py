@@ -444,6 +444,15 @@ def main():
                                          "FP64_PEAK_TFS / FP32_PEAK_TFS, measured by scripts/valu_peak.hip)"),
                                 "hbm": {k: hbm[k] for k in ("achieved", "peak", "unit", "frac", "bytes_per_walker_step")}}
             line["pairs_per_s"] = round(pairs / (head_ms * 1e-3), 1)
+        floor_path = os.path.join(ROOT, "profiles", "r03_launch_floor.json")
+        if N <= 16384 and os.path.exists(floor_path):
+            # a small batch is one wave's latency chain per launch: state the launch floor it is bounded by
+            # (scripts/launch_floor.hip on a box: the same 128 x 256 geometry, back-to-back launches, HIP events)
+            fl = json.load(open(floor_path))
+            line["floor"] = {"empty_launch_us": fl["empty_us"], "load_store_launch_us": fl["load1_us"],
+                             "step_over_load_store": round(step_ms * 1e3 / fl["load1_us"], 3),
+                             "source": "profiles/r03_launch_floor.json (scripts/launch_floor.hip): back-to-back "
+                                       "launches of an empty kernel and of one coalesced load + store per lane"}
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.workload, params, args.chain_points, args.cpu_seconds)
         print(json.dumps(line), flush=True)

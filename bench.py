@@ -414,10 +414,11 @@ def main():
         if closed_ms is not None:
             line["closed_loop"] = {
                 "ms_per_step": round(closed_ms, 5), "env_steps_per_s": round(N * 1e3 / closed_ms, 1),
-                "lanes": env._lanes(None),
+                "lanes": env._step_lanes(),
                 "note": "BatchedPhysicsEnv.step() once per env step (HIP events on the calling stream over 20-200 "
-                        "steps): the walker ranges join every step and each step returns obs / reward / done / info "
-                        "— what a policy loop gets; `value` is the open-loop rate (K steps issued back to back)"}
+                        "steps; one walker range, step()'s default): each step returns obs / reward / done / info "
+                        "— what a PhysicsEnv.step caller gets; `value` is the open-loop rate (K steps issued back "
+                        "to back on the ranges of run())"}
         if resident_ms is not None:
             line["resident_rollout"] = {
                 "ms_per_step": round(resident_ms, 5), "env_steps_per_s": round(N * 1e3 / resident_ms, 1),

@@ -3,7 +3,7 @@
 (gym/optimized_env.py:53-92: reset -> step(action) -> (obs, reward, done, info)), here on the MI355X
 stepper (one launch per step; the reference's own demo.py is empty).
 
-    python demo.py [--env Balance-v0|Box-v0] [--steps 200] [--seed 0] [--g1 insect]
+    python demo.py [--env Balance-v0|Box-v0] [--steps 200] [--seed 0] [--g1 leg2]
 
 ``--g1 NAME`` runs one of the G1 builders (gym/walker.py:138-353, walker_gym_amd.topologies) through the
 legacy ``Environment(...).step(t)`` API (gym/env.py:48-50) instead.

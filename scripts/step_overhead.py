@@ -26,9 +26,11 @@ def main():
     T = 200
     for lanes in ("1", "2"):
         os.environ["WG_LANES"] = lanes
+        os.environ["WG_STEP_LANES"] = lanes
         env = BatchedPhysicsEnv(spec, device="cuda:0", **params)
         A = max(1, env.batch.A)
         acts = (torch.rand((T, n, A), device="cuda:0") * 2 - 1).contiguous()
+        env.run(acts, T, lanes=int(lanes))    # warm: the clocks up before anything is timed
         for s in range(10):
             env.step(acts[s])
         torch.cuda.synchronize()
@@ -61,6 +63,7 @@ def main():
             pstats.Stats(pr, stream=buf).sort_stats("tottime").print_stats(12)
             res["profile_lanes2"] = buf.getvalue().splitlines()[:40]
     del os.environ["WG_LANES"]
+    del os.environ["WG_STEP_LANES"]
     line = json.dumps(res)
     print(line)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)

@@ -83,3 +83,18 @@ def test_make_env_unknown_id_raises():
     from walker_gym_amd.optimized_env import make_env
     with pytest.raises(ValueError, match="Unknown environment ID"):
         make_env("Walker-v9", device="cuda:0")
+
+
+@pytest.mark.parametrize("args,head", [(["--steps", "60"], "Balance-v0: "), (["--env", "Box-v0", "--steps", "30"], "Box-v0: "),
+                                       (["--g1", "leg2", "--steps", "20"], "leg2: 20 steps")])
+def test_demo_runs(args, head):
+    """BASELINE config 0 (one walker through the gym API, demo.py) runs end to end on the GPU stepper."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "demo.py")] + args, capture_output=True, text=True,
+                       timeout=180, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = r.stdout.strip().splitlines()[-1]
+    assert line.startswith(head), line
+    assert "nan" not in line.lower(), line

@@ -267,7 +267,7 @@ class BatchedPhysicsEnv:
         cached = getattr(self, "_plan_cache", None)
         if cached is not None and cached["key"] == key:
             return cached
-        lanes = self._lanes(None) if cols >= 0 else 1
+        lanes = self._step_lanes() if cols >= 0 else 1
         self.reserve_streams(lanes)
         b = self.batch
         keep = []                                  # the ctypes structs the ranges point at
@@ -386,6 +386,15 @@ class BatchedPhysicsEnv:
         if self.batch.ragged:
             return max(1, min(lanes, self.batch.plan_blocks // 64))
         return 1 if self.N < 64 * lanes else lanes
+
+    def _step_lanes(self) -> int:
+        """Walker ranges of step(): 1 unless WG_STEP_LANES says otherwise.  step() joins its ranges at the end of
+        every call, so a second range cannot fill the first one's launch tail with its next step (what pays in
+        run()), and the fork / join events cost host time on every call: measured on the canonical 65,536-walker
+        batch, a step() loop ran 47.7 us per step with 1 range against 58.5 with 2 (host 7.8 against 25.1 us per
+        call; scripts/step_overhead.py, profiles/r03g_step_overhead_canonical.json)."""
+        env = os.environ.get("WG_STEP_LANES")
+        return self._lanes(int(env)) if env else 1
 
     def reserve_streams(self, lanes: int) -> None:
         """Side streams for `lanes` walker ranges (lanes - 1 of them; existing ones are kept, so their hardware

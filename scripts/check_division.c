@@ -1,5 +1,6 @@
 /* Host check of the exact-division identities the HIP kernel relies on (walker_hip.hip fdiv_exact /
- * ddiv_exact): float x/m == (float)((double)x * RN64(1/m)) and Markstein's corrected double quotient.
+ * ddiv_exact / fdiv_count): float x/m == (float)((double)x * RN64(1/m)), Markstein's corrected double
+ * quotient, and x / M for an integer M from a reciprocal within two ulps.
  * Usage: check_division [n]   (prints mismatch counts; all must be 0). */
 #include <stdio.h>
 #include <stdlib.h>
@@ -44,5 +45,29 @@ int main(int argc, char** argv){
     if ((float)((double)x*ym) != x/m) b4++;
   }
   printf("adversarial bad=%ld\n", b4);
-  return (bad1||bad2||bad3||b4) ? 1 : 0;
+  /* (5) fdiv_count: float x / M for an integer M < 2^11 as (float)(x * y), y within two ulps of 1/M (rcp64_nr),
+   * |x| >= 2^-100: random x over the whole exponent range, and x = M * (a float rounding midpoint) nudged */
+  long b5=0, n5=0;
+  for (long i=0;i<n/4;i++){
+    const int M = 1 + (int)(xr()%2047);
+    const double y0 = 1.0/(double)M;
+    const double ys[5] = {y0, nextafter(y0,0), nextafter(y0,1), nextafter(nextafter(y0,0),0), nextafter(nextafter(y0,1),1)};
+    float x;
+    if (i & 1) { uint32_t ux = (uint32_t)xr(); memcpy(&x,&ux,4); }
+    else {
+      const uint64_t k = (xr() & 0xffffffull) | 0x1000001ull;           /* 25-bit odd significand: a midpoint */
+      const double mid = (double)k * ldexp(1.0, -(int)(xr()%200) + 60);
+      x = (float)(mid * (double)M);
+      const int nudge = (int)(xr()%5) - 2;
+      for (int j=0;j<nudge;j++) x = nextafterf(x, INFINITY);
+      for (int j=0;j>nudge;j--) x = nextafterf(x, -INFINITY);
+      if (xr() & 1) x = -x;
+    }
+    if (!isfinite(x) || !(fabsf(x) >= 0x1p-100f)) continue;
+    const float ref = x/(float)M;
+    n5++;
+    for (int j=0;j<5;j++) if ((float)((double)x*ys[j]) != ref) b5++;
+  }
+  printf("count-divisor n=%ld bad=%ld\n", n5, b5);
+  return (bad1||bad2||bad3||b4||b5) ? 1 : 0;
 }

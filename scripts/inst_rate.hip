@@ -118,6 +118,61 @@ U64(k_rcp_f64, "v_rcp_f64")
 U64(k_sqrt_f64, "v_sqrt_f64")
 CVT2(k_cvt, "v_cvt_f64_f32", "v_cvt_f32_f64")
 
+// dependent chains (one chain per lane): launched with one wave per SIMD they give the issue-to-issue latency of a
+// dependent instruction; with W waves per SIMD, how far W waves interleaving one chain each get towards the issue rate
+__global__ __launch_bounds__(256) void d_fma_f32(uint32_t *out, uint32_t yy) {
+    float x = threadIdx.x, y = (float)yy;
+    for (int i = 0; i < ITERS; i++)
+        asm volatile("v_fma_f32 %0, %0, %1, %1\n\tv_fma_f32 %0, %0, %1, %1\n\tv_fma_f32 %0, %0, %1, %1\n\t"
+                     "v_fma_f32 %0, %0, %1, %1\n\tv_fma_f32 %0, %0, %1, %1\n\tv_fma_f32 %0, %0, %1, %1\n\t"
+                     "v_fma_f32 %0, %0, %1, %1\n\tv_fma_f32 %0, %0, %1, %1" : "+v"(x) : "v"(y));
+    if (x == 12345.678f) out[threadIdx.x] = 1;
+}
+__global__ __launch_bounds__(256) void d_fma_f64(uint32_t *out, uint32_t yy) {
+    double x = threadIdx.x, y = (double)yy;
+    for (int i = 0; i < ITERS; i++)
+        asm volatile("v_fma_f64 %0, %0, %1, %1\n\tv_fma_f64 %0, %0, %1, %1\n\tv_fma_f64 %0, %0, %1, %1\n\t"
+                     "v_fma_f64 %0, %0, %1, %1\n\tv_fma_f64 %0, %0, %1, %1\n\tv_fma_f64 %0, %0, %1, %1\n\t"
+                     "v_fma_f64 %0, %0, %1, %1\n\tv_fma_f64 %0, %0, %1, %1" : "+v"(x) : "v"(y));
+    if (x == 12345.678) out[threadIdx.x] = 1;
+}
+// the mass loop's accumulation step a = f32(f64(a) + q) followed by the damping add, as one dependent chain of 4
+__global__ __launch_bounds__(256) void d_acc(uint32_t *out, uint32_t yy) {
+    float a = threadIdx.x, g = (float)yy;
+    double q = (double)yy, t;
+    for (int i = 0; i < ITERS; i++)
+        asm volatile("v_cvt_f64_f32 %1, %0\n\tv_add_f64 %1, %1, %2\n\tv_cvt_f32_f64 %0, %1\n\tv_add_f32 %0, %0, %3\n\t"
+                     "v_cvt_f64_f32 %1, %0\n\tv_add_f64 %1, %1, %2\n\tv_cvt_f32_f64 %0, %1\n\tv_add_f32 %0, %0, %3"
+                     : "+v"(a), "=&v"(t) : "v"(q), "v"(g));
+    if (a == 12345.678f) out[threadIdx.x] = 1;
+}
+// DPP row_shr:1 add chain (the per-walker sequential sums)
+__global__ __launch_bounds__(256) void d_dpp(uint32_t *out, uint32_t yy) {
+    float x = threadIdx.x, y = (float)yy;
+    for (int i = 0; i < ITERS; i++)
+        asm volatile("v_add_f32_dpp %0, %0, %1 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+                     "v_add_f32_dpp %0, %0, %1 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+                     "v_add_f32_dpp %0, %0, %1 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+                     "v_add_f32_dpp %0, %0, %1 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+                     "v_add_f32_dpp %0, %0, %1 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+                     "v_add_f32_dpp %0, %0, %1 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+                     "v_add_f32_dpp %0, %0, %1 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+                     "v_add_f32_dpp %0, %0, %1 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "+v"(x) : "v"(y));
+    if (x == 12345.678f) out[threadIdx.x] = 1;
+}
+// ds_bpermute throughput: 8 independent gathers per iteration (the spring phase's endpoint gathers)
+__global__ __launch_bounds__(256) void k_bperm(uint32_t *out, uint32_t yy) {
+    int a = (threadIdx.x ^ yy) << 2, v0 = threadIdx.x, v1 = v0 + 1, v2 = v0 + 2, v3 = v0 + 3, v4 = v0 + 4, v5 = v0 + 5,
+        v6 = v0 + 6, v7 = v0 + 7;
+    for (int i = 0; i < ITERS; i++) {
+        v0 = __builtin_amdgcn_ds_bpermute(a, v0); v1 = __builtin_amdgcn_ds_bpermute(a, v1);
+        v2 = __builtin_amdgcn_ds_bpermute(a, v2); v3 = __builtin_amdgcn_ds_bpermute(a, v3);
+        v4 = __builtin_amdgcn_ds_bpermute(a, v4); v5 = __builtin_amdgcn_ds_bpermute(a, v5);
+        v6 = __builtin_amdgcn_ds_bpermute(a, v6); v7 = __builtin_amdgcn_ds_bpermute(a, v7);
+    }
+    if ((v0 ^ v1 ^ v2 ^ v3 ^ v4 ^ v5 ^ v6 ^ v7) == 0x12345678) out[threadIdx.x] = 1;
+}
+
 typedef void (*kfn)(uint32_t *, uint32_t);
 struct Kind { const char *name; kfn k; double per_iter; };   // per_iter: instructions per chain iteration
 
@@ -160,6 +215,33 @@ int main() {
            clk_ghz);
     for (int v = 0; v < nk; v++)
         printf("%s\"%s\": %.2f", v ? ", " : "", kinds[v].name, 4.0 * ms_per_inst[v] / ref);
+    printf("}");
+    // dependent chains at W waves per SIMD (W workgroups of 4 waves per CU): SIMD cycles per chain instruction per
+    // wave, at the clock implied above (cycles between two dependent instructions of one wave when W = 1)
+    const Kind deps[] = {{"dep v_fma_f32", d_fma_f32, 8}, {"dep v_fma_f64", d_fma_f64, 8},
+                         {"dep cvt+add_f64+cvt+add_f32 (per instruction)", d_acc, 8},
+                         {"dep v_add_f32_dpp row_shr", d_dpp, 8}, {"ds_bpermute_b32 (8 independent)", k_bperm, 8}};
+    printf(", \"dependent_chain_cycles_per_instruction\": {");
+    for (int v = 0; v < (int)(sizeof(deps) / sizeof(deps[0])); v++) {
+        printf("%s\"%s\": {", v ? ", " : "", deps[v].name);
+        const int ws[] = {1, 2, 4, 6, 8};
+        for (int wi = 0; wi < 5; wi++) {
+            float best = 1e30f;
+            for (int rep = 0; rep < 4; rep++) {
+                CK(hipEventRecord(e0));
+                hipLaunchKernelGGL(deps[v].k, dim3(pr.multiProcessorCount * ws[wi]), dim3(256), 0, 0, d, 3u);
+                CK(hipEventRecord(e1));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                if (rep > 0 && ms < best) best = ms;
+            }
+            // one SIMD runs ws waves, each ITERS * per_iter instructions in its chain: cycles per (wave, instruction)
+            const double cyc = best * 1e-3 * clk_ghz * 1e9 / (ITERS * deps[v].per_iter);
+            printf("%s\"w%d\": %.2f", wi ? ", " : "", ws[wi], cyc / ws[wi]);
+        }
+        printf("}");
+    }
     printf("}}\n");
     return 0;
 }

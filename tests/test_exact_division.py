@@ -14,3 +14,4 @@ def test_exact_division_identities(tmp_path):
     assert r.returncode == 0, r.stdout
     assert "bad f32-via-f64=0 markstein(t/m)=0 markstein(fv/c)=0" in r.stdout
     assert "adversarial bad=0" in r.stdout
+    assert "count-divisor" in r.stdout and r.stdout.rstrip().endswith("bad=0")

@@ -290,6 +290,23 @@ __device__ __forceinline__ double rcp64_nr(double d) {
     return __builtin_fma(y, e, y);
 }
 
+// numpy's float32 x / M for a walker's mass count M (np.mean's final division; 1 <= M < 2^20):
+// (float)(x * y) with y = rcp64_nr(M) (within about an ulp of 1/M).  When x / M is a normal float, it is either
+// representable or at least 2^-25 / M (relative) from every float rounding midpoint (a midpoint has a 25-bit odd
+// significand), while the double product is within 2^-50 of x / M: the conversion rounds it exactly as the IEEE
+// division would.  |x| < 2^-100 (a possibly subnormal quotient, where that spacing argument fails) takes the
+// IEEE division, in a branch.  3 VALU instead of the ~11 of a correctly rounded float32 division.  Checked on the
+// host for M < 2^11 with reciprocals up to two ulps off (scripts/check_division.c, tests/test_exact_division.py).
+#ifndef WG_FAST_MEAN
+#define WG_FAST_MEAN 1
+#endif
+__device__ __forceinline__ float fdiv_count(float x, float fM, double yM) {
+    if (!WG_FAST_MEAN) return x / fM;
+    float q = (float)((double)x * yM);
+    if (__builtin_expect(__builtin_fabsf(x) < 0x1p-100f, 0)) q = x / fM;
+    return q;
+}
+
 // sqrtf of a float s in [2^-96, 2^126): v_sqrt_f32 and the one-ulp correction, the same steps as the compiler's
 // correctly rounded sqrtf minus its small-input rescaling and zero/inf fix-up, which this range never needs
 __device__ __forceinline__ float sqrt_mid(float s) {
@@ -583,6 +600,81 @@ __device__ __forceinline__ void mass_accumulate(const TS &ts, const uint16_t *in
                 ay = ay + fxsign(q.f1 / mf, sd);
                 az = az + fxsign(q.f2 / mf, sd);
             }
+        }
+    }
+}
+
+// The barrier-free kernels' mass loop (spring_mode 0), with the per-entry bookkeeping cut to five VALU: an entry
+// (edge << 1 | end) addresses its term records as tb + 24 * edge and fb + 12 * edge (two v_mad_u32_u24 from the
+// walker's term bases), its end's sign is one v_lshl_or_b32 into the float64 and one into the float32 +-1 (the
+// damping takes the opposite sign through the fma's neg modifier), and the list is walked by pointer with no
+// clamp on the read-ahead: the entries after a mass's list are the next mass's, and the tile's last list is
+// followed by a zero word (the wave writes one after its incidence words), so every read-ahead is a valid entry
+// whose values go unused.  Arithmetic and its order are those of acc_f64_entry<true> (bit-identical).
+#ifndef WG_MASS_V2
+#define WG_MASS_V2 1
+#endif
+__device__ __forceinline__ IncTerm inc_term_at(const char *tb, const char *fb, uint32_t ent) {
+    const uint32_t e = ent >> 1;
+    const double *t = reinterpret_cast<const double *>(tb + __umul24(e, 24u));
+    const float *f = reinterpret_cast<const float *>(fb + __umul24(e, 12u));
+    return IncTerm{t[0], t[1], t[2], f[0], f[1], f[2]};
+}
+__device__ __forceinline__ void acc_entry_v2(const IncTerm &q, uint32_t ent, double md, double ym, float mf, float ymf,
+                                             float &ax, float &ay, float &az) {
+    // +1 at end i, -1 at end j, as the float64's high word and as a float32 (the damping takes -sgf); one
+    // v_lshl_or_b32 each (the compiler would share one shift between two ors)
+    uint32_t hi, sf;
+    asm("v_lshl_or_b32 %0, %1, 31, %2" : "=v"(hi) : "v"(ent), "s"(0x3ff00000u));
+    asm("v_lshl_or_b32 %0, %1, 31, %2" : "=v"(sf) : "v"(ent), "s"(0x3f800000u));
+    const double sgn = __hiloint2double((int)hi, 0);
+    const float sgf = __uint_as_float(sf);
+    ax = (float)__builtin_fma(ddiv_fast(q.t0, md, ym), sgn, (double)ax);
+    ay = (float)__builtin_fma(ddiv_fast(q.t1, md, ym), sgn, (double)ay);
+    az = (float)__builtin_fma(ddiv_fast(q.t2, md, ym), sgn, (double)az);
+    ax = __builtin_fmaf(fdiv_fast(q.f0, mf, ymf), -sgf, ax);
+    ay = __builtin_fmaf(fdiv_fast(q.f1, mf, ymf), -sgf, ay);
+    az = __builtin_fmaf(fdiv_fast(q.f2, mf, ymf), -sgf, az);
+}
+// ym = RN64(1/m) from the caller (one IEEE division per mass, shared with the env forces)
+__device__ __forceinline__ void mass_accumulate_v2(const TermsAoS &ts, const uint16_t *inc, int lb, int s0, int s1,
+                                                   float mf, double ym, float &ax, float &ay, float &az) {
+    const double md = (double)mf;
+    const float ymf = (float)ym;      // = RN32(1/m)
+    ax = 0.f; ay = 0.f; az = 0.f;
+    const char *tb = reinterpret_cast<const char *>(ts.t + 3 * lb), *fb = reinterpret_cast<const char *>(ts.f + 3 * lb);
+    if (s1 > s0) {
+        const uint16_t *p = inc + s0;
+        uint32_t ea = p[0], eb = p[1];
+        IncTerm A = inc_term_at(tb, fb, ea), B;
+        for (int r = s0; r < s1; r += 2) {
+            B = inc_term_at(tb, fb, eb);
+            const uint32_t ea2 = p[2];
+            __builtin_amdgcn_sched_barrier(0);   // keep the reads above the arithmetic
+            acc_entry_v2(A, ea, md, ym, mf, ymf, ax, ay, az);
+            if (r + 1 >= s1) break;
+            A = inc_term_at(tb, fb, ea2);
+            const uint32_t eb2 = p[3];
+            __builtin_amdgcn_sched_barrier(0);
+            acc_entry_v2(B, eb, md, ym, mf, ymf, ax, ay, az);
+            ea = ea2; eb = eb2; p += 2;
+            asm volatile("" : "+v"(A.t0), "+v"(A.t1), "+v"(A.t2), "+v"(A.f0), "+v"(A.f1), "+v"(A.f2));
+        }
+    }
+    // a non-finite sum: some quotient was not exact (or an input not finite); redo the list with IEEE divisions
+    if (__builtin_expect(!(__builtin_isfinite(ax) && __builtin_isfinite(ay) && __builtin_isfinite(az)), 0)) {
+        ax = 0.f; ay = 0.f; az = 0.f;
+        for (int r = s0; r < s1; r++) {
+            const int ent = inc[r];
+            const uint32_t sj = (uint32_t)(ent & 1) << 31;
+            const IncTerm q = ts.get(lb + (ent >> 1));
+            ax = (float)((double)ax + dxsign(q.t0 / md, sj));
+            ay = (float)((double)ay + dxsign(q.t1 / md, sj));
+            az = (float)((double)az + dxsign(q.t2 / md, sj));
+            const uint32_t sd = sj ^ 0x80000000u;
+            ax = ax + fxsign(q.f0 / mf, sd);
+            ay = ay + fxsign(q.f1 / mf, sd);
+            az = az + fxsign(q.f2 / mf, sd);
         }
     }
 }
@@ -1765,6 +1857,7 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
 #pragma unroll
         for (int it = 0; it < NE; it++)
             if (lane + 64 * it < nE) s_inc[lane + 64 * it] = L.gi[it];
+        if (WG_MASS_V2 && lane == 0) s_inc[nE] = 0u;   // the read-ahead pad after the last list (mass_accumulate_v2)
     }
     float x = L.x;
     if (acts) {
@@ -1774,7 +1867,9 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
         if (store) b.muscle_x[ul] = x;
     }
     if (is_mus) s_x[lane] = x;
-    const double ym = 1.0 / (double)mf;   // IEEE 1/m of this lane's mass: every /m below is exact from it
+    double ym = 1.0 / (double)mf;   // IEEE 1/m of this lane's mass: every /m below is exact from it
+    // (opaque: otherwise the compiler turns (float)ym, which is RN32(1/m), into a second, float32 IEEE division)
+    if (WG_MASS_V2 && !RES) asm volatile("" : "+v"(ym));
     wave_sync();
     STAMP(2);
 
@@ -1833,8 +1928,11 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
         const int r1 = (WG_ABLATE & 2) ? min(L.io1, L.io0 + 1) : L.io1;
         const int lb = wl * K;
         // (the resident kernel keeps the XOR sign form: 5 fewer registers where its carried state is live)
-        mass_accumulate<LeanTerms, !RES>(ts, reinterpret_cast<const uint16_t *>(s_inc) + 2 * lb, lb, L.io0, r1, mf, ax,
-                                         ay, az, 0);
+        if (WG_MASS_V2 && !RES)
+            mass_accumulate_v2(ts, reinterpret_cast<const uint16_t *>(s_inc) + 2 * lb, lb, L.io0, r1, mf, ym, ax, ay, az);
+        else
+            mass_accumulate<LeanTerms, !RES>(ts, reinterpret_cast<const uint16_t *>(s_inc) + 2 * lb, lb, L.io0, r1, mf,
+                                             ax, ay, az, 0);
     }
     // every lane (gathers); the resident kernel runs pair-free batches only (wg_rollout falls back to wg_step)
     if (!RES && kp.pair_mode) pair_forces(b, kp, L.p3, mf, pl, lane, M, is_mass, ax, ay, az);
@@ -2166,6 +2264,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
 #pragma unroll
     for (int it = 0; it < NE; it++)
         if (lane + 64 * it < nE) s_inc[lane + 64 * it] = gi[it];
+    if (WG_MASS_V2 && lane == 0) s_inc[nE] = 0u;   // the read-ahead pad after the last list (mass_accumulate_v2)
     float x = mx;
     if (acts) {
         x = (kp.action_mode == 1) ? ((act != 0.f) ? x + mst : x - mst) : x + act;
@@ -2174,7 +2273,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
         b.muscle_x[U0 + lane] = x;
     }
     if (is_mus) s_x[lane] = x;
-    const double ym = 1.0 / (double)mf;
+    double ym = 1.0 / (double)mf;
+    if (WG_MASS_V2) asm volatile("" : "+v"(ym));   // (float)ym stays a conversion, not a float32 division
     wave_sync();
     STAMP(2);
 
@@ -2204,8 +2304,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
     float px = 0.f, py = 0.f, pz = 0.f, vx = 0.f, vy = 0.f, vz = 0.f, ax = 0.f, ay = 0.f, az = 0.f;
     bool hit = false;
     if (is_mass) {
-        mass_accumulate<TermsAoS, true>(ts, reinterpret_cast<const uint16_t *>(s_inc) + 2 * mlb, mlb, io0, io1, mf, ax,
-                                            ay, az, 0);
+        if (WG_MASS_V2)
+            mass_accumulate_v2(ts, reinterpret_cast<const uint16_t *>(s_inc) + 2 * mlb, mlb, io0, io1, mf, ym, ax, ay, az);
+        else
+            mass_accumulate<TermsAoS, true>(ts, reinterpret_cast<const uint16_t *>(s_inc) + 2 * mlb, mlb, io0, io1, mf,
+                                            ax, ay, az, 0);
         mass_tail(kp, mf, (float)ym, p3, v3, px, py, pz, vx, vy, vz, ax, ay, az, hit, pin != 0);
         const uint32_t pl = (uint32_t)(P0 + lane);
         float *gpo = b.pos + 3 * (size_t)pl, *gvo = b.vel + 3 * (size_t)pl, *gao = b.acc + 3 * (size_t)pl;
@@ -2252,13 +2355,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
     if (lane < nw) {
         const int M = s_mo[lane + 1] - s_mo[lane];
         const float fM = (float)M;
+        const double yM = rcp64_nr((double)M);
         const float *rd = s_red + 8 * lane;
-        const float cy = rd[3] / fM;
+        const float cy = fdiv_count(rd[3], fM, yM);
         const int packed = __float_as_int(rd[7]);
         const int hits = packed >> 1, all = packed & 1;
         const int steps = wsteps + 1;
         b.steps[w0 + lane] = steps;
-        if (o.reward) o.reward[wrow] = (cy + (-(rd[4] / fM)) * 0.1f) + (float)(-(double)hits * 0.5);
+        if (o.reward) o.reward[wrow] = (cy + (-fdiv_count(rd[4], fM, yM)) * 0.1f) + (float)(-(double)hits * 0.5);
         if (o.done) {
             int done = steps >= kp.max_steps;
             if (!done && cy < kp.done_y) done = 1;
@@ -2266,7 +2370,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
             o.done[wrow] = (uint8_t)done;
         }
         if (o.centroid) {
-            o.centroid[3 * wrow] = rd[0] / fM; o.centroid[3 * wrow + 1] = rd[1] / fM; o.centroid[3 * wrow + 2] = rd[2] / fM;
+            o.centroid[3 * wrow] = fdiv_count(rd[0], fM, yM); o.centroid[3 * wrow + 1] = fdiv_count(rd[1], fM, yM);
+            o.centroid[3 * wrow + 2] = fdiv_count(rd[2], fM, yM);
         }
         if (o.energy) o.energy[wrow] = 0.5f * rd[5] + rd[6];
     }
@@ -2283,12 +2388,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
         if (is_mass) {
             const float *rd = s_red + 8 * mw;
             const float fM = (float)mM;
+            const double yM = rcp64_nr((double)mM);
             float *dst = o.obs + (size_t)s_row[mw] * stride + per * (lane - mlm);
             const float pm[3] = {px, py, pz}, vm[3] = {vx, vy, vz}, am[3] = {ax, ay, az};
             fvd vp, vv, va;
 #pragma unroll
             for (int c = 0; c < d; c++) {
-                const float mid = kp.midform == 2 ? rd[c] : rd[c] / fM;   // G1 getstat: the SUM
+                const float mid = kp.midform == 2 ? rd[c] : fdiv_count(rd[c], fM, yM);   // G1 getstat: the SUM
                 vp[c] = kp.midform ? (pm[c] - mid) * kp.pk : pm[c] * kp.pk;
                 vv[c] = vm[c] * kp.vk;
                 va[c] = am[c] * kp.ak;
@@ -2534,7 +2640,7 @@ bool lean_geo(const wg_batch *b, int obs_stride, LeanGeo *out, int spring_mode =
     // t (f64 x3) | df (f32 x3) | incidence words | x (observation rows go from registers to HBM, no LDS tile)
     g.off_df = align16(g.pl * 24);
     g.off_inc = g.off_df + align16(g.pl * 12);
-    g.off_x = g.off_inc + align16(ew * 4);
+    g.off_x = g.off_inc + align16(ew * 4 + 4);              // + the zero word after the last list (mass_accumulate_v2)
     g.slice = g.off_x + align16(std::max(1, g.wpw * b->A) * 4);
     if (4 * g.slice > 80 * 1024) return false;
     g.invK = 1.f / (float)b->K;
@@ -2619,7 +2725,7 @@ bool rag_geo(const wg_batch *b, int obs_stride, RagGeo *out) {
     // incidence words | muscle x | walker offsets and rows
     g.off_df = align16(std::max(ec * 24, 4 * 64 * 6));
     g.off_inc = g.off_df + align16(std::max(ec * 12, 4 * RW_MAXW * 8));
-    g.off_x = g.off_inc + align16(ec * 4);
+    g.off_x = g.off_inc + align16(ec * 4 + 4);                   // + the read-ahead pad word (mass_accumulate_v2)
     g.off_wo = g.off_x + align16(64 * 4);
     g.slice = g.off_wo + align16(4 * (RW_MAXW + 1) * 3 + 4 * RW_MAXW);
     *out = g;

@@ -761,13 +761,26 @@ __device__ inline float seq_sum_quad(float x) {
     a = a + quad_bcast<2>(x);
     return a + quad_bcast<3>(x);
 }
+#ifndef WG_SEQ3
+#define WG_SEQ3 1
+#endif
 __device__ inline void seq_sum3_lanes(float x, float y, float z, int base, int M, float &sx, float &sy, float &sz) {
     float a, b, c;
     if (M == 4) {
         sx = seq_sum_quad(x); sy = seq_sum_quad(y); sz = seq_sum_quad(z);
         return;
     }
-    if (M <= 16) {            // walkers of M | 16 lanes sit inside one 16-lane DPP row
+    if (WG_SEQ3 && M == 16) {
+        // the three chains interleaved in one unrolled body (three independent DPP adds per step instead of one chain
+        // at a time behind a scalar loop); the empty asm keeps each chain's adds scalar (no SLP packing, which has
+        // no DPP form)
+        a = 0.f + x; b = 0.f + y; c = 0.f + z;
+#pragma unroll
+        for (int t = 1; t < 16; t++) {
+            a = dpp_f<0x111>(a) + x; b = dpp_f<0x111>(b) + y; c = dpp_f<0x111>(c) + z;
+            asm volatile("" : "+v"(a), "+v"(b), "+v"(c));
+        }
+    } else if (M <= 16) {     // walkers of M | 16 lanes sit inside one 16-lane DPP row
         a = seq_chain<0x111>(x, M); b = seq_chain<0x111>(y, M); c = seq_chain<0x111>(z, M);
     } else {
         a = seq_chain<0x138>(x, M); b = seq_chain<0x138>(y, M); c = seq_chain<0x138>(z, M);
@@ -801,6 +814,63 @@ __device__ inline float pw_sum_lanes(float x, int base, int M, int lane) {
     r = r + __shfl_xor(r, 4, 64);
     return r;
 }
+
+// All seven per-walker sums of the observe step (lane values -> per-walker totals): the sequential sums of x, y, z
+// (getstat's mid, info's centroid) and numpy's pairwise sums of y (np.mean), |v|, m|v|^2, m g (y - ground).  For
+// M = 4 and M = 16 (Balance-v0 / Box-v0 and the canonical walker) the seven chains run interleaved in one
+// straight-line block — every DPP add has six independent ones to fill its wait states, where the generic path
+// (M known only at run time) runs each sum behind its own branches — with the same additions in the same order.
+#ifndef WG_SUMS7
+#define WG_SUMS7 1
+#endif
+struct WalkerSums { float sx, sy, sz, ysum, vsum, ksum, psum; };
+#define WG_OPAQUE7(a, b, c, d, e, f, g) asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e), "+v"(f), "+v"(g))
+__device__ inline WalkerSums walker_sums(float px, float py, float pz, float nv, float ke, float pe, int base, int M,
+                                         int lane) {
+    WalkerSums r;
+    if (WG_SUMS7 && M == 4) {
+        // a walker is one DPP quad: every lane adds the quad's four values in order (M < 8: pairwise == sequential)
+        float a = 0.f + quad_bcast<0>(px), b = 0.f + quad_bcast<0>(py), c = 0.f + quad_bcast<0>(pz);
+        float d = 0.f + quad_bcast<0>(nv), e = 0.f + quad_bcast<0>(ke), f = 0.f + quad_bcast<0>(pe);
+        WG_OPAQUE7(a, b, c, d, e, f, py);
+        a = a + quad_bcast<1>(px); b = b + quad_bcast<1>(py); c = c + quad_bcast<1>(pz);
+        d = d + quad_bcast<1>(nv); e = e + quad_bcast<1>(ke); f = f + quad_bcast<1>(pe);
+        WG_OPAQUE7(a, b, c, d, e, f, py);
+        a = a + quad_bcast<2>(px); b = b + quad_bcast<2>(py); c = c + quad_bcast<2>(pz);
+        d = d + quad_bcast<2>(nv); e = e + quad_bcast<2>(ke); f = f + quad_bcast<2>(pe);
+        WG_OPAQUE7(a, b, c, d, e, f, py);
+        a = a + quad_bcast<3>(px); b = b + quad_bcast<3>(py); c = c + quad_bcast<3>(pz);
+        d = d + quad_bcast<3>(nv); e = e + quad_bcast<3>(ke); f = f + quad_bcast<3>(pe);
+        r.sx = a; r.sy = b; r.sz = c; r.ysum = b; r.vsum = d; r.ksum = e; r.psum = f;
+        return r;
+    }
+    if (WG_SUMS7 && M == 16) {
+        // sequential: s_q <- s_{q-1} + x_q along the row (lane base + 15 ends with the walker's left-to-right sum);
+        // pairwise: r_j = x_j + x_{j+8}, then ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) by quad_perm / half-mirror moves
+        float a = 0.f + px, b = 0.f + py, c = 0.f + pz;
+        float y = py + dpp_f<0x128>(py), v = nv + dpp_f<0x128>(nv), k = ke + dpp_f<0x128>(ke), e = pe + dpp_f<0x128>(pe);
+        WG_OPAQUE7(a, b, c, y, v, k, e);
+        y = y + dpp_f<0xB1>(y); v = v + dpp_f<0xB1>(v); k = k + dpp_f<0xB1>(k); e = e + dpp_f<0xB1>(e);
+        WG_OPAQUE7(a, b, c, y, v, k, e);
+        y = y + dpp_f<0x4E>(y); v = v + dpp_f<0x4E>(v); k = k + dpp_f<0x4E>(k); e = e + dpp_f<0x4E>(e);
+        WG_OPAQUE7(a, b, c, y, v, k, e);
+        y = y + dpp_f<0x141>(y); v = v + dpp_f<0x141>(v); k = k + dpp_f<0x141>(k); e = e + dpp_f<0x141>(e);
+#pragma unroll
+        for (int t = 1; t < 16; t++) {
+            a = dpp_f<0x111>(a) + px; b = dpp_f<0x111>(b) + py; c = dpp_f<0x111>(c) + pz;
+            asm volatile("" : "+v"(a), "+v"(b), "+v"(c));
+        }
+        const int last = base + 15;
+        r.sx = lane_get(a, last); r.sy = lane_get(b, last); r.sz = lane_get(c, last);
+        r.ysum = y; r.vsum = v; r.ksum = k; r.psum = e;
+        return r;
+    }
+    seq_sum3_lanes(px, py, pz, base, M, r.sx, r.sy, r.sz);
+    r.ysum = pw_sum_lanes(py, base, M, lane); r.vsum = pw_sum_lanes(nv, base, M, lane);
+    r.ksum = pw_sum_lanes(ke, base, M, lane); r.psum = pw_sum_lanes(pe, base, M, lane);
+    return r;
+}
+#undef WG_OPAQUE7
 
 // ------------------------------------------------------------------ pair terms
 #ifndef WG_FAST_PAIR
@@ -1947,10 +2017,8 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
 
     // ================= per-walker reductions (wave shuffles) + outputs (gym/optimized_env.py:189-248)
     const int gbase = lane & ~(M - 1);
-    float sx, sy, sz;
-    seq_sum3_lanes(px, py, pz, gbase, M, sx, sy, sz);
-    const float ysum = pw_sum_lanes(py, gbase, M, lane), vsum = pw_sum_lanes(nv, gbase, M, lane);
-    const float ksum = pw_sum_lanes(ke, gbase, M, lane), psum = pw_sum_lanes(pe, gbase, M, lane);
+    const WalkerSums ws = walker_sums(px, py, pz, nv, ke, pe, gbase, M, lane);
+    const float sx = ws.sx, sy = ws.sy, sz = ws.sz, ysum = ws.ysum, vsum = ws.vsum, ksum = ws.ksum, psum = ws.psum;
     const unsigned long long gmask = (M == 64) ? ~0ull : (((1ull << M) - 1ull) << gbase);
     const unsigned long long hb = __ballot(is_mass && (py - kp.ground < 0.f));   // contacts after run1 (:200)
     const unsigned long long sb = __ballot(is_mass && nv < 0.1f);

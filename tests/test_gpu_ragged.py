@@ -297,3 +297,44 @@ def test_out_of_cap_wave_plan_is_skipped_and_reported():
     torch.cuda.synchronize()
     assert L.wg_plan_errors(1) == 1 and L.wg_plan_errors(0) == 0
     assert torch.equal(env.pos, pos0)
+
+
+@pytest.mark.gpu
+def test_info_steps_caller_order_without_gather():
+    """A permuted (ragged) batch's info['steps'] comes from the kernels' caller-order steps output (wg_outputs.steps,
+    ABI 9) after step() / run() / observe(), and from a gather after rollout() or loaded state: equal to the stored
+    counters in the caller's order either way."""
+    import torch
+    from walker_gym_amd.batched_env import BatchedPhysicsEnv
+    from walker_gym_amd.synthetic import ragged_walkers
+    N = 700
+    spec = ragged_walkers(N, seed=21, mmin=4, mmax=30)
+    A = int(np.max(spec["n_muscles"]))
+    env = BatchedPhysicsEnv(spec, device="cuda:0", in3d=1)
+    assert env.steps_out is not None
+    acts = torch.rand((6, N, A), device="cuda:0") * 2 - 1
+
+    def check(expect_out):
+        info = env.info()
+        torch.cuda.synchronize()
+        ref = env.batch.caller("steps")
+        assert torch.equal(info["steps"], ref)
+        assert (info["steps"].data_ptr() == env.steps_out.data_ptr()) == expect_out
+        return ref
+
+    for t in range(3):
+        env.step(acts[t])
+    assert (check(True) == 3).all()
+    env.run(acts[3:5].contiguous(), 2)
+    assert (check(True) == 5).all()
+    env.rollout(acts[:2])
+    assert (check(False) == 7).all()
+    mask = torch.zeros(N, dtype=torch.uint8, device="cuda:0")
+    mask[::3] = 1
+    env.reset(mask=mask)
+    got = check(True)
+    assert (got[::3] == 0).all() and (got[1::3] == 7).all()
+    sd = env.batch.state_dict()
+    env.step(acts[5])
+    env.batch.load_state_dict(sd)
+    assert torch.equal(check(False), got)

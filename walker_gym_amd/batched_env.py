@@ -180,13 +180,17 @@ class BatchedPhysicsEnv:
         self.done = torch.zeros(N, dtype=torch.bool, device=dv)
         self.centroid = torch.zeros((N, 3), dtype=torch.float32, device=dv)
         self.energy = torch.zeros(N, dtype=torch.float32, device=dv)
+        # info['steps'] of a permuted (ragged) batch in the caller's order, written by the step kernels themselves
+        # (wg_outputs.steps) so that step() needs no gather; valid while _steps_at == the batch's state version
+        self.steps_out = torch.zeros(N, dtype=torch.int32, device=dv) if self.batch._perm else None
+        self._steps_at = -1
 
     def _outputs(self, obs=None, reward=None, done=None, centroid=None, energy=None, obs_step=0, out_step=0,
-                 pad_clean=False):
+                 pad_clean=False, steps=None):
         p = lambda t: None if t is None else C.c_void_p(t.data_ptr())
         return _lib.WgOutputs(obs=p(obs), obs_stride=self.obs_dim, reward=p(reward), done=p(done),
                               centroid=p(centroid), energy=p(energy), obs_step=obs_step, out_step=out_step,
-                              obs_pad_clean=int(pad_clean))
+                              obs_pad_clean=int(pad_clean), steps=p(steps))
 
     def _stream(self):
         return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
@@ -254,6 +258,7 @@ class BatchedPhysicsEnv:
                         plan["events"])
         if rc:
             _lib.check(rc, "wg_step_ranges")
+        self._steps_at = self.batch.version
         if act is not None and plan["n"] > 1:
             for st in plan["side"]:
                 act.record_stream(st)   # the allocator must not recycle the actions before the side streams read them
@@ -275,7 +280,8 @@ class BatchedPhysicsEnv:
 
         def out(w0, w1):
             o = self._outputs(self.obs[w0:w1], self.reward[w0:w1], self.done[w0:w1], self.centroid[w0:w1],
-                              self.energy[w0:w1], pad_clean=True)
+                              self.energy[w0:w1], pad_clean=True,
+                              steps=None if self.steps_out is None else self.steps_out[w0:w1])
             keep.append(o)
             return C.pointer(o)
         if lanes == 1 or b.ragged:
@@ -318,6 +324,7 @@ class BatchedPhysicsEnv:
             raise ValueError("actions must be [T, N, A]")
         T, _, cols = actions.shape
         dv = self.device
+        self._steps_at = -1   # the step counters move without the steps output: info() gathers them afterwards
         # zero-filled: a ragged batch's short rows then need only their own values written each step
         clean = obs_out is None
         obs_out = torch.zeros((T, self.N, self.obs_dim), dtype=torch.float32, device=dv) if obs_out is None else obs_out
@@ -357,17 +364,24 @@ class BatchedPhysicsEnv:
             raise ValueError("actions must be a contiguous [n_steps or 1, N, A] device tensor")
         lanes = self._lanes(1 if (resident and lanes is None and self.resident_ok()) else lanes)
         entry = "wg_rollout" if resident else "wg_step"
+        so = self.steps_out if info else None
         if lanes > 1:
-            return self._run_lanes(actions, int(n_steps), lambda w0, w1: self._outputs(
+            self._run_lanes(actions, int(n_steps), lambda w0, w1: self._outputs(
                 self.obs[w0:w1], self.reward[w0:w1], self.done[w0:w1], self.centroid[w0:w1] if info else None,
-                self.energy[w0:w1] if info else None, pad_clean=True), lanes, entry=entry)
+                self.energy[w0:w1] if info else None, pad_clean=True, steps=None if so is None else so[w0:w1]),
+                lanes, entry=entry)
+            self._steps_at = self.batch.version if so is not None else -1
+            return
         o = self._outputs(self.obs, self.reward, self.done, self.centroid if info else None,
-                          self.energy if info else None, pad_clean=True)
+                          self.energy if info else None, pad_clean=True, steps=so)
         _lib.check(getattr(_lib.load(), entry)(
             C.byref(self.batch.struct), C.byref(self._pstruct), C.c_void_p(actions.data_ptr()), cols, cols,
             0 if T == 1 else self.N * cols, C.byref(o), int(n_steps),
             None if self.batch.plan is None else C.c_void_p(self.batch.plan.data_ptr()),
             self.batch.plan_blocks, self._stream()), entry)
+        # (a resident launch writes the steps output only where the resident kernel runs: uniform batches, which
+        # have no steps_out)
+        self._steps_at = self.batch.version if so is not None else -1
 
     def _lanes(self, lanes: Optional[int]) -> int:
         """Walker ranges run() steps on separate streams (ragged batches: ranges of plan blocks).  Default 2 for
@@ -461,11 +475,12 @@ class BatchedPhysicsEnv:
         return WalkerGraph(self, g, actions)
 
     def observe(self):
-        o = self._outputs(self.obs, self.reward, self.done, self.centroid, self.energy)
+        o = self._outputs(self.obs, self.reward, self.done, self.centroid, self.energy, steps=self.steps_out)
         _lib.check(_lib.load().wg_observe(
             C.byref(self.batch.struct), C.byref(self._pstruct), C.byref(o),
             None if self.batch.plan is None else C.c_void_p(self.batch.plan.data_ptr()),
             self.batch.plan_blocks, self._stream()), "wg_observe")
+        self._steps_at = self.batch.version
         return self.obs, self.reward, self.done, self.info()
 
     def reset(self, noise=None, mask=None):
@@ -490,12 +505,17 @@ class BatchedPhysicsEnv:
         return [seed] if seed is not None else []
 
     def info(self) -> dict:
-        return {"steps": self.batch.caller("steps"), "centroid_position": self.centroid, "total_energy": self.energy}
+        if self.steps_out is not None and self._steps_at == self.batch.version:
+            steps = self.steps_out                 # written by the last step / observe in caller order
+        else:
+            steps = self.batch.caller("steps")     # a gather (after a rollout, a reset mask, or loaded state)
+        return {"steps": steps, "centroid_position": self.centroid, "total_energy": self.energy}
 
     # state accessors in the caller's order.  An unpermuted batch returns live views into its tensors; a ragged batch
     # (stored in wave-tile / size order) returns gathered COPIES, so in-place writes into them do not reach the batch:
     # assign instead (env.pos = t, env.vel[...] edits then env.vel = edited), which scatters into the stored order.
     def _set_state(self, name: str, value) -> None:
+        self.batch.version += 1
         dst = getattr(self.batch, name)
         t = torch.as_tensor(value, dtype=dst.dtype).to(self.device).reshape(dst.shape)
         dst.copy_(self.batch.to_stored(self.batch.KIND[name], t))

@@ -1357,6 +1357,7 @@ __global__ __launch_bounds__(MAXT) void walker_step_kernel(
             const size_t wg = (size_t)(w0 + my_wl);
             int steps = wsteps;
             if (STEP) { steps += 1; b.steps[wg] = steps; }
+            if (o.steps) o.steps[wg] = steps;
             const float cy = ysum / fM;
             if (o.reward) {
                 const float vpen = (-(vsum / fM)) * 0.1f;
@@ -1422,6 +1423,7 @@ __global__ __launch_bounds__(MAXT) void walker_step_kernel(
             const int hits = packed >> 1, all = packed & 1;
             int steps = wsteps;
             if (STEP) { steps += 1; b.steps[ws] = steps; }
+            if (o.steps) o.steps[wg] = steps;
             if (o.reward) {
                 const float av = rd[4] / fM;
                 const float vpen = (-av) * 0.1f;
@@ -2037,6 +2039,7 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
             const int steps = L.wsteps + 1;
             if (store) b.steps[wg] = steps;
             if (RES) L.wsteps = steps;
+            if (o.steps) o.steps[wg] = steps;
             const float cy = ysum * lg.invM;
             if (o.reward) {
                 const float vpen = (-(vsum * lg.invM)) * 0.1f;
@@ -2177,6 +2180,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
         if (os.done) os.done += (size_t)s * os.out_step;
         if (os.energy) os.energy += (size_t)s * os.out_step;
         if (os.centroid) os.centroid += 3 * (size_t)s * os.out_step;
+        if (os.steps) os.steps += (size_t)s * os.out_step;
         // the same for the static inputs (the mass's 1/m, the springs' endpoint indices are re-derived per step)
         asm volatile("" : "+v"(L.mf), "+v"(L.io0), "+v"(L.io1), "+v"(L.lo), "+v"(L.hi), "+v"(L.stp));
 #pragma unroll
@@ -2430,6 +2434,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
         const int hits = packed >> 1, all = packed & 1;
         const int steps = wsteps + 1;
         b.steps[w0 + lane] = steps;
+        if (o.steps) o.steps[wrow] = steps;
         if (o.reward) o.reward[wrow] = (cy + (-fdiv_count(rd[4], fM, yM)) * 0.1f) + (float)(-(double)hits * 0.5);
         if (o.done) {
             int done = steps >= kp.max_steps;
@@ -2886,6 +2891,7 @@ int run(const wg_batch *b, const wg_params *p, const float *action, int32_t cols
         if (os.done) os.done += s * os.out_step;
         if (os.energy) os.energy += s * os.out_step;
         if (os.centroid) os.centroid += 3 * s * os.out_step;
+        if (os.steps) os.steps += s * os.out_step;
         const float *a = action ? action + s * astep : nullptr;
         if (step && use_lean) {
             rc = launch_lean(b, kp, p->in3d != 0, a, cols, astride, os, lg, stream);

@@ -74,6 +74,7 @@ class DeviceBatch:
         self.plan = None
         self.plan_blocks = 0
         self.ragged_kind = 0
+        self.version = 0   # bumped by every host-side write of the state (load_state_dict, setters, reset)
         self.replan(wave_ok)
 
     def replan(self, wave_ok: bool) -> None:
@@ -211,6 +212,7 @@ class DeviceBatch:
 
     def load_state_dict(self, sd: dict) -> None:
         """Inverse of state_dict: caller-order tensors copied into the stored order."""
+        self.version += 1
         for k in self.STATE:
             getattr(self, k).copy_(self.to_stored(self.KIND[k], sd[k].to(self.device)))
         if "radius" in sd:

@@ -2408,7 +2408,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
     // ================= per-walker reductions, 8 lanes per walker (numpy's summation orders) ==========
     // r 0-2: sequential sums of pos[:, r] (getstat mid / info centroid); r 3: pairwise y (np.mean);
     // r 4-6: pairwise |v|, m|v|^2, m*g*(y - ground); r 7: contact count << 1 | all-stopped, from the ballots
-    for (int idx = lane; idx < nw * 8; idx += 64) {
+    for (int idx = lane; idx < ((WG_ABLATE & 32) ? 0 : nw * 8); idx += 64) {   // (ablation bit 32: no reductions)
         const int w = idx >> 3, r = idx & 7;
         const int lm = s_mo[w], M = s_mo[w + 1] - lm;
         float v;

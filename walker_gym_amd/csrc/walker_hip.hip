@@ -1038,43 +1038,58 @@ __device__ void pair_electrostatic_lds(const wg_batch &b, const KParams &kp, con
 }
 
 // Mass q of the walker whose masses are LDS [lm, lm + M) and global [g0, g0 + M).
+// One central-force pass of the workgroup kernel (GRAV: Point.gravity with s = m from LDS; else Point.coulomb with s
+// = the charge): mass q meets its partners in ascending index, the strengths in the reference pair's (i < j) order.
+template <bool GRAV>
+__device__ __forceinline__ void pair_central_pass_lds(const wg_batch &b, double coef, double sq, const float *spos,
+                                                      const float *sm, int lm, int M, int q, size_t g0, double pe,
+                                                      double md, double ym, const float *p3, float &ax, float &ay,
+                                                      float &az) {
+    auto strength = [&](int pj) -> double {
+        return GRAV ? (double)sm[lm + pj] : (b.charge ? (double)b.charge[g0 + pj] : pe);
+    };
+    const float sx = ax, sy = ay, sz = az;
+    bool bad = !WG_FAST_PAIR;
+    if (WG_FAST_PAIR && M > 0) {
+        const float *o3 = spos + 3 * lm;
+        float n0 = o3[0], n1 = o3[1], n2 = o3[2];
+        double ns = strength(0);
+        for (int pj = 0; pj < M; pj++) {
+            const float c0 = n0, c1 = n1, c2 = n2;
+            const double os = ns;
+            const int nx = min(pj + 1, M - 1);                  // (the last read repeats partner M - 1, unused)
+            n0 = o3[3 * nx]; n1 = o3[3 * nx + 1]; n2 = o3[3 * nx + 2];
+            ns = strength(nx);
+            if (pj == q) continue;
+            pair_central_fast(coef, pj < q ? os : sq, pj < q ? sq : os, c0 - p3[0], c1 - p3[1], c2 - p3[2], md, ym,
+                              ax, ay, az, bad);
+        }
+        bad = bad || !__builtin_isfinite(ax + ay + az);
+    }
+    if (__builtin_expect(bad, 0)) {   // the exact pass: IEEE divisions and sqrtf
+        ax = sx; ay = sy; az = sz;
+        for (int pj = 0; pj < M; pj++) {
+            if (pj == q) continue;
+            const float *o3 = spos + 3 * (lm + pj);
+            const double os = strength(pj);
+            pair_central_term(coef, pj < q ? os : sq, pj < q ? sq : os, o3[0] - p3[0], o3[1] - p3[1], o3[2] - p3[2],
+                              md, ym, ax, ay, az);
+        }
+    }
+}
+
 __device__ void pair_forces_lds(const wg_batch &b, const KParams &kp, const float *spos, const float *sm, int lm,
                                 int M, int q, size_t g0, float mf, float &ax, float &ay, float &az) {
     const float *p3 = spos + 3 * (lm + q);
     const double md = (double)mf;
     const double ym = 1.0 / md;                  // every "/ m" below: ddiv_f32d (m is a float32 value)
-    for (int pass = 0; pass < 2; pass++) {   // gym/engine.py:128-137 (Config.g, m) and :139-147 (Config.k, e)
-        if (!(kp.pair_mode & (1 << pass))) continue;
-        const double coef = pass == 0 ? kp.pair_g : kp.pair_k;
-        const double sq = pass == 0 ? md : (b.charge ? b.charge[g0 + q] : kp.pair_e);
-        auto partner = [&](int pj, double &os, float &d0, float &d1, float &d2) {
-            const float *o3 = spos + 3 * (lm + pj);
-            os = pass == 0 ? (double)sm[lm + pj] : (b.charge ? b.charge[g0 + pj] : kp.pair_e);
-            d0 = o3[0] - p3[0]; d1 = o3[1] - p3[1]; d2 = o3[2] - p3[2];   // partner - self
-        };
-        const float sx = ax, sy = ay, sz = az;
-        bool bad = !WG_FAST_PAIR;
-        if (WG_FAST_PAIR) {
-            for (int pj = 0; pj < M; pj++) {
-                if (pj == q) continue;
-                double os;
-                float d0, d1, d2;
-                partner(pj, os, d0, d1, d2);
-                pair_central_fast(coef, pj < q ? os : sq, pj < q ? sq : os, d0, d1, d2, md, ym, ax, ay, az, bad);
-            }
-            bad = bad || !__builtin_isfinite(ax + ay + az);
-        }
-        if (__builtin_expect(bad, 0)) {   // the exact pass: IEEE divisions and sqrtf
-            ax = sx; ay = sy; az = sz;
-            for (int pj = 0; pj < M; pj++) {
-                if (pj == q) continue;
-                double os;
-                float d0, d1, d2;
-                partner(pj, os, d0, d1, d2);
-                pair_central_term(coef, pj < q ? os : sq, pj < q ? sq : os, d0, d1, d2, md, ym, ax, ay, az);
-            }
-        }
-    }
+    // gym/engine.py:128-137 (Config.g, m) and :139-147 (Config.k, e): one loop per pass, each partner's state read one
+    // partner ahead (the term of partner pj computes while pj + 1's position and strength are in flight)
+    if (kp.pair_mode & 1)
+        pair_central_pass_lds<true>(b, kp.pair_g, md, spos, sm, lm, M, q, g0, 0.0, md, ym, p3, ax, ay, az);
+    if (kp.pair_mode & 2)
+        pair_central_pass_lds<false>(b, kp.pair_k, b.charge ? (double)b.charge[g0 + q] : kp.pair_e, spos, sm, lm, M, q,
+                                     g0, kp.pair_e, md, ym, p3, ax, ay, az);
     if (kp.pair_mode & 4) {                  // gym/engine.py:114-125, partners j < q, then j != q, then j > q
         const double rs = b.radius[g0 + q];
         for (int ph = 0; ph < 3; ph++) {

@@ -1124,8 +1124,18 @@ __device__ void pair_forces_lds(const wg_batch &b, const KParams &kp, const floa
 // ------------------------------------------------------------------ the step kernel
 // STEP = false: observe only (reset path).  RAGGED: CSR offsets + block plan.  IN3D: obs layout.
 // PWD: pairwise-sum recursion depth (0: M <= 128).  SHFL: register reductions (uniform, M | 64).
+// Register budget of the step instances with the unrolled-once pairwise tree (PWD 0, no lane shuffles): 6 waves per
+// SIMD, i.e. 80 VGPRs, so three 512-thread workgroups share a CU instead of two (the compiler's own choice, 90 VGPRs,
+// is 5 waves per SIMD, which a 512-thread workgroup rounds down to 4): 4,096 chains of 100 masses 159.6 -> 153.8 us
+// per launch, the performance_demo loop 181.9 -> 173.4 (profiles/r03v_ab_wg_occupancy.json); 7 spills more and
+// gains less.  The PWD 3 and shuffle instances would spill 48-116 B at 80 VGPRs and keep the compiler's choice.
+#ifndef WG_WG_OCC
+#define WG_WG_OCC 6
+#endif
 template <bool STEP, bool RAGGED, bool IN3D, int PWD, bool SHFL>
-__global__ __launch_bounds__(MAXT) void walker_step_kernel(
+constexpr int wg_kernel_waves() { return (STEP && PWD == 0 && !SHFL && WG_WG_OCC) ? WG_WG_OCC : 1; }
+template <bool STEP, bool RAGGED, bool IN3D, int PWD, bool SHFL>
+__global__ __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(wg_kernel_waves<STEP, RAGGED, IN3D, PWD, SHFL>()))) void walker_step_kernel(
     wg_batch b, KParams kp, const float *__restrict__ action, int action_cols, int action_stride,
     wg_outputs o, const int32_t *__restrict__ plan, Geo geo) {
     extern __shared__ __attribute__((aligned(16))) char smem[];

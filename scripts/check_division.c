@@ -69,5 +69,29 @@ int main(int argc, char** argv){
     for (int j=0;j<5;j++) if ((float)((double)x*ys[j]) != ref) b5++;
   }
   printf("count-divisor n=%ld bad=%ld\n", n5, b5);
-  return (bad1||bad2||bad3||b4||b5) ? 1 : 0;
+  /* (6) the float32 quotients' exact range (walker_hip.hip TINY_EXP / divisor_ok): dividend 0 or |x| >= 2^-80, divisor
+   * |m| in [2^-20, 2^21), finite quotient: Markstein's float32 step from RN32(1/m), the double product with RN64(1/m)
+   * (fdiv_exact) and with a reciprocal two ulps off (fdiv_rcp from rcp64_nr) all equal IEEE x / m.  Dividends drawn
+   * over the whole range and concentrated near its low end, divisors near the range's ends too. */
+  long b6=0, n6=0;
+  for (long i=0;i<n/2;i++){
+    uint32_t ux=(uint32_t)xr(); int ex = (i & 1) ? 127-80+(int)(xr()%208) : 127-80+(int)(xr()%24);
+    if (ex > 254) continue;
+    ux=(ux&0x807fffffu)|((uint32_t)ex<<23); float x; memcpy(&x,&ux,4);
+    if (xr()%64==0) x = 0.0f;
+    uint32_t um=(uint32_t)xr(); int em = (i & 2) ? 127-20+(int)(xr()%41) : ((i & 4) ? 127-20+(int)(xr()%3) : 127+18+(int)(xr()%3));
+    um=(um&0x007fffffu)|((uint32_t)em<<23); float m; memcpy(&m,&um,4);
+    if (xr()&1) m = -m;
+    const float ref = x/m;
+    if (!isfinite(ref)) continue;
+    n6++;
+    const float yf = (float)(1.0/(double)m);
+    const float q = x*yf, r = fmaf(-q, m, x), qm = fmaf(r, yf, q);
+    if (memcmp(&qm,&ref,4)) b6++;
+    const double y0 = 1.0/(double)m;
+    const double ys[3] = {y0, nextafter(nextafter(y0,0),0), nextafter(nextafter(y0,INFINITY),INFINITY)};
+    for (int j=0;j<3;j++){ const float qd=(float)((double)x*ys[j]); if (memcmp(&qd,&ref,4)) b6++; }
+  }
+  printf("exact-range n=%ld bad=%ld\n", n6, b6);
+  return (bad1||bad2||bad3||b4||b5||b6) ? 1 : 0;
 }

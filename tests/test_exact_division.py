@@ -14,4 +14,6 @@ def test_exact_division_identities(tmp_path):
     assert r.returncode == 0, r.stdout
     assert "bad f32-via-f64=0 markstein(t/m)=0 markstein(fv/c)=0" in r.stdout
     assert "adversarial bad=0" in r.stdout
-    assert "count-divisor" in r.stdout and r.stdout.rstrip().endswith("bad=0")
+    assert "count-divisor" in r.stdout and "count-divisor n=" in r.stdout
+    lines = {l.split()[0]: l for l in r.stdout.splitlines()}
+    assert lines["count-divisor"].endswith("bad=0") and lines["exact-range"].endswith("bad=0")

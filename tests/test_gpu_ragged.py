@@ -338,3 +338,36 @@ def test_info_steps_caller_order_without_gather():
     env.step(acts[5])
     env.batch.load_state_dict(sd)
     assert torch.equal(check(False), got)
+
+
+@pytest.mark.gpu
+def test_tiny_and_subnormal_means_exact():
+    """The wave kernel's per-walker means go through fdiv_count (an exact reciprocal product) except for |sum| <
+    2^-100, which takes the IEEE division: walkers whose x coordinates are scaled to ~1e-36 (normal, tiny means) and
+    ~1e-40 (subnormal coordinates and means) give the workgroup kernel's (IEEE) and the oracle's bits."""
+    import torch
+    from oracle.oracle import Oracle
+    from walker_gym_amd.batched_env import BatchedPhysicsEnv
+    from walker_gym_amd.synthetic import ragged_walkers
+    N = 400
+    spec = ragged_walkers(N, seed=77, mmin=3, mmax=40)
+    mo = spec["mass_off"]
+    for w in range(N):
+        spec["pos"][mo[w]:mo[w + 1], 0] *= np.float32(1e-36 if w % 2 else 1e-40)
+    A = int(np.max(spec["n_muscles"]))
+    acts = np.random.default_rng(77).uniform(-1, 1, (6, N, A)).astype(np.float32)
+    env, wave = _rollout(spec, dict(in3d=1), acts, lean=True)
+    assert env.batch.ragged_kind == 2
+    _, wg = _rollout(spec, dict(in3d=1), acts, lean=False)
+    for x, y in zip(wave, wg):
+        assert np.array_equal(x.view(np.uint8), y.view(np.uint8))
+    env = BatchedPhysicsEnv(spec, device="cuda:0", in3d=1)
+    orc = Oracle(spec, dict(in3d=1))
+    for t in range(3):
+        obs, rew, done, info = env.step(acts[t])
+        ref = orc.step(acts[t])
+    torch.cuda.synchronize()
+    cen = info["centroid_position"].cpu().numpy()
+    assert (np.abs(cen[:, 0]) < 1e-30).all() and (np.abs(cen[0::2, 0]) < 1.2e-38).any()   # subnormal means reached
+    assert np.array_equal(cen.view(np.uint32), ref["centroid"].view(np.uint32))
+    assert np.array_equal(obs.cpu().numpy().view(np.uint32), ref["obs"].view(np.uint32))

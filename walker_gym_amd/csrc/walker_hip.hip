@@ -240,11 +240,26 @@ __device__ inline int fdiv(int idx, int d, float inv) {
 //    final correction step: y within 1/2 ulp of 1/b and q within 1 ulp of a/b -> correctly rounded).
 // Non-finite operands take the plain expression (the correction would turn inf into NaN).
 __device__ inline float fdiv_exact(float x, double y) { return (float)((double)x * y); }
+// The operand range of the float32 quotients (Markstein's step below, and the double products fdiv_exact /
+// fdiv_rcp): exact when the dividend is 0 or at least 2^-80 in magnitude and the divisor lies in [2^-20, 2^21), the
+// result being finite (scripts/check_division.c case 6, 300 M random operands).  Below that the Markstein residual
+// or the quotient itself leaves the normal range (x / m misrounds for some |x| < 2^-105), and a
+// double product rounded to a subnormal float can sit on a rounding midpoint.  fexp is frexp's exponent (0 for 0,
+// inf and NaN: zero dividends pass), so one min over fexp's tests a whole set of dividends.
+constexpr int TINY_EXP = -79;   // fexp(x) >= TINY_EXP  <=>  x == 0 or |x| >= 2^-80
+__device__ __forceinline__ int fexp(float x) { return __builtin_amdgcn_frexp_expf(x); }
+__device__ __forceinline__ int fexp3(float a, float b, float c) { return min(min(fexp(a), fexp(b)), fexp(c)); }
+__device__ __forceinline__ bool divisor_ok(float m) {   // m in [2^-20, 2^21) in magnitude
+    const int e = fexp(m);
+    return e >= -19 && e <= 21 && m != 0.f;
+}
 //  * float x / float m == fmaf(fmaf(-q, m, x), yf, q) with yf = RN32(1/m) = (float)RN64(1/m),
-//    q = RN32(x*yf): the same Markstein step in binary32 (3 f32 ops, no f64 issue slots).
+//    q = RN32(x*yf): the same Markstein step in binary32 (3 f32 ops, no f64 issue slots), for operands in the range
+//    above; outside it (and for a zero, infinite or NaN divisor or quotient) the IEEE division.
 __device__ inline float fdiv_mk(float x, float m, float yf) {
     const float q = x * yf;
     if (!__builtin_isfinite(q) || yf == 0.f) return q;
+    if (__builtin_expect(fexp(x) < TINY_EXP || !divisor_ok(m), 0)) return x / m;
     return __builtin_fmaf(__builtin_fmaf(-q, m, x), yf, q);
 }
 __device__ inline float fxsign(float v, uint32_t s) { return __uint_as_float(__float_as_uint(v) ^ s); }
@@ -361,8 +376,9 @@ __device__ inline bool edge_string(uint32_t ij) { return (ij >> 31) != 0u; }
 //   spring  gym/engine.py:78-102 resilience (two anti_forced calls, float64 force path, :73-75)
 //   damping gym/optimized_walker.py:92-106 (float32), the same expression for every element type
 // spring_mode 1 = the G2 element as written (gym/optimized_walker.py:48-60: float32, inverted sign).
+// gt: the damping force has a component below the exact range of the mass loop's float32 quotient (fexp < TINY_EXP)
 __device__ __forceinline__ void spring_edge(const EdgeRec &e, int le, int lm, float x, const float *spos,
-                                            const float *svel, double *st, float *sdf, int spring_mode) {
+                                            const float *svel, double *st, float *sdf, int spring_mode, bool &gt) {
     const int i = lm + edge_i(e.ij), j = lm + edge_j(e.ij);
     const float pix = spos[3 * i], piy = spos[3 * i + 1], piz = spos[3 * i + 2];
     const float pjx = spos[3 * j], pjy = spos[3 * j + 1], pjz = spos[3 * j + 2];
@@ -400,7 +416,9 @@ __device__ __forceinline__ void spring_edge(const EdgeRec &e, int le, int lm, fl
         t1 = ddiv_fast((double)(nf * r1), dist, yc);
         t2 = ddiv_fast((double)(nf * r2), dist, yc);
     }
-    const bool fast_ok = cur > 0.f && (double)cur == dist && __builtin_isfinite(d0) && __builtin_isfinite(d1) &&
+    // (the quotients d = r / cur are exact for r in the operand range and cur in [2^-20, 2^20))
+    const bool fast_ok = cur >= 0x1p-20f && cur < 0x1p20f && fexp3(r0, r1, r2) >= TINY_EXP &&
+                         (double)cur == dist && __builtin_isfinite(d0) && __builtin_isfinite(d1) &&
                          __builtin_isfinite(d2) && __builtin_isfinite(t0) && __builtin_isfinite(t1) &&
                          __builtin_isfinite(t2);
     if (__builtin_expect(!fast_ok, 0)) {
@@ -416,6 +434,7 @@ __device__ __forceinline__ void spring_edge(const EdgeRec &e, int le, int lm, fl
     const float dk = np_dot3(vix - vjx, viy - vjy, viz - vjz, d0, d1, d2);  // :102-103
     const float dkc = dk * e.c;                                               // :104
     sdf[3 * le] = dkc * d0; sdf[3 * le + 1] = dkc * d1; sdf[3 * le + 2] = dkc * d2;
+    gt = gt || fexp3(sdf[3 * le], sdf[3 * le + 1], sdf[3 * le + 2]) < TINY_EXP;
 }
 
 // One incidence entry's spring term (float64) and damping force (float32), read from LDS.
@@ -471,24 +490,32 @@ __device__ __forceinline__ void acc_f64_entry(const IncTerm &q, int ent, double 
 // the caller then redoes the forces with the guarded ones (fdiv_mk, which equal IEEE division).
 template <bool FAST>
 __device__ __forceinline__ float fdiv_env(float x, float m, float y) { return FAST ? fdiv_fast(x, m, y) : fdiv_mk(x, m, y); }
+// emin (FAST): the least fexp over the dividends, for the caller's exact-range test.
 template <bool FAST>
 __device__ __forceinline__ void env_forces(const KParams &kp, float mf, float ymf, float vx, float vy, float vz,
-                                           float py, float &ax, float &ay, float &az, bool &hit) {
+                                           float py, float &ax, float &ay, float &az, bool &hit, int &emin) {
     const float zm = fdiv_mk(0.f, mf, ymf);   // the zero components of the env forces, divided by m
     // gravity [0,-g,0]/m, damp -dampk*v/m  (gym/env.py:32-33, optimized_env.py:148-151)
+    const float dvx = kp.neg_dampk * vx, dvy = kp.neg_dampk * vy, dvz = kp.neg_dampk * vz;
+    if (FAST) {
+        emin = fexp(kp.neg_g);
+        if (kp.neg_dampk != 0.f) emin = min(emin, fexp3(dvx, dvy, dvz));   // (a zero damping makes them zeros)
+    }
     ax = ax + zm; ay = ay + fdiv_env<FAST>(kp.neg_g, mf, ymf); az = az + zm;
-    ax = ax + fdiv_env<FAST>(kp.neg_dampk * vx, mf, ymf);
-    ay = ay + fdiv_env<FAST>(kp.neg_dampk * vy, mf, ymf);
-    az = az + fdiv_env<FAST>(kp.neg_dampk * vz, mf, ymf);
+    ax = ax + fdiv_env<FAST>(dvx, mf, ymf);
+    ay = ay + fdiv_env<FAST>(dvy, mf, ymf);
+    az = az + fdiv_env<FAST>(dvz, mf, ymf);
     const float deep = py - kp.ground;
     hit = deep < 0.f;                                                // optimized_env.py:154
     if (hit) {
-        ax = ax + zm; ay = ay + fdiv_env<FAST>(kp.neg_groundk * deep, mf, ymf); az = az + zm;
-        ax = ax + zm; ay = ay + fdiv_env<FAST>(kp.neg_grounddamp * vy, mf, ymf); az = az + zm;
+        const float gk = kp.neg_groundk * deep, gd = kp.neg_grounddamp * vy;
+        ax = ax + zm; ay = ay + fdiv_env<FAST>(gk, mf, ymf); az = az + zm;
+        ax = ax + zm; ay = ay + fdiv_env<FAST>(gd, mf, ymf); az = az + zm;
         const float ff = fabsf(deep) * kp.friction;                  // :168
         // G1 env (gym/env.py:41): [v_x*deep*friction, 0, v_z*deep*friction], left to right in float32
         const float fx = kp.friction_mode ? (vx * deep) * kp.friction : (-vx) * ff;
         const float fz = kp.friction_mode ? (vz * deep) * kp.friction : (-vz) * ff;
+        if (FAST) emin = min(emin, min(fexp3(gk, gd, fx), fexp(fz)));
         ax = ax + fdiv_env<FAST>(fx, mf, ymf); ay = ay + zm; az = az + fdiv_env<FAST>(fz, mf, ymf);
     }
 }
@@ -503,13 +530,16 @@ __device__ __forceinline__ void mass_tail(const KParams &kp, float mf, float ymf
     px = p3[0]; py = p3[1]; pz = p3[2];
     if (WG_FAST_ENV) {
         const float sx = ax, sy = ay, sz = az;
-        env_forces<true>(kp, mf, ymf, vx, vy, vz, py, ax, ay, az, hit);
-        if (__builtin_expect(!__builtin_isfinite(ax + ay + az), 0)) {   // cold: redo with exact quotients
+        int emin = 0;
+        env_forces<true>(kp, mf, ymf, vx, vy, vz, py, ax, ay, az, hit, emin);
+        // cold: redo with exact quotients (a non-finite sum, a dividend or the mass outside the exact range)
+        if (__builtin_expect(!__builtin_isfinite(ax + ay + az) || emin < TINY_EXP || !divisor_ok(mf), 0)) {
             ax = sx; ay = sy; az = sz;
-            env_forces<false>(kp, mf, ymf, vx, vy, vz, py, ax, ay, az, hit);
+            env_forces<false>(kp, mf, ymf, vx, vy, vz, py, ax, ay, az, hit, emin);
         }
     } else {
-        env_forces<false>(kp, mf, ymf, vx, vy, vz, py, ax, ay, az, hit);
+        int emin = 0;
+        env_forces<false>(kp, mf, ymf, vx, vy, vz, py, ax, ay, az, hit, emin);
     }
     if (pinned) { ax = 0.f; ay = 0.f; az = 0.f; }   // DingPoint.forced is a no-op: a stays zeros()
     // v += a*t in both integrators; the position update differs (a wave-uniform branch on the parameter, on
@@ -535,7 +565,7 @@ __device__ __forceinline__ void mass_tail(const KParams &kp, float mf, float ymf
 // Point.forced), then Point.run1 (gym/engine.py:174-178).  Returns the new state and old_a.
 template <class TS, bool FMA_SIGN = true>
 __device__ __forceinline__ void mass_accumulate(const TS &ts, const uint16_t *inc, int lb, int s0, int s1, float mf,
-                                                float &ax, float &ay, float &az, int spring_mode) {
+                                                float &ax, float &ay, float &az, int spring_mode, bool force = false) {
     const double md = (double)mf;
     const double ym = 1.0 / md;      // one IEEE division per mass; every /m below is exact from it
     const float ymf = (float)ym;     // = RN32(1/m)
@@ -584,7 +614,10 @@ __device__ __forceinline__ void mass_accumulate(const TS &ts, const uint16_t *in
                 asm volatile("" : "+v"(A.t0), "+v"(A.t1), "+v"(A.t2), "+v"(A.f0), "+v"(A.f1), "+v"(A.f2), "+v"(ea), "+v"(eb));
             }
         }
-        const bool bad = !(__builtin_isfinite(ax) && __builtin_isfinite(ay) && __builtin_isfinite(az));
+        // force: a damping force of the tile outside the exact range of the float32 quotient (the caller's flag), or a
+        // mass outside its divisor range
+        const bool bad = force || !divisor_ok(mf) ||
+                         !(__builtin_isfinite(ax) && __builtin_isfinite(ay) && __builtin_isfinite(az));
         if (__builtin_expect(bad, 0)) {
             ax = 0.f; ay = 0.f; az = 0.f;
             for (int r = s0; r < s1; r++) {
@@ -638,7 +671,7 @@ __device__ __forceinline__ void acc_entry_v2(const IncTerm &q, uint32_t ent, dou
 }
 // ym = RN64(1/m) from the caller (one IEEE division per mass, shared with the env forces)
 __device__ __forceinline__ void mass_accumulate_v2(const TermsAoS &ts, const uint16_t *inc, int lb, int s0, int s1,
-                                                   float mf, double ym, float &ax, float &ay, float &az) {
+                                                   float mf, double ym, float &ax, float &ay, float &az, bool force) {
     const double md = (double)mf;
     const float ymf = (float)ym;      // = RN32(1/m)
     ax = 0.f; ay = 0.f; az = 0.f;
@@ -661,8 +694,10 @@ __device__ __forceinline__ void mass_accumulate_v2(const TermsAoS &ts, const uin
             asm volatile("" : "+v"(A.t0), "+v"(A.t1), "+v"(A.t2), "+v"(A.f0), "+v"(A.f1), "+v"(A.f2));
         }
     }
-    // a non-finite sum: some quotient was not exact (or an input not finite); redo the list with IEEE divisions
-    if (__builtin_expect(!(__builtin_isfinite(ax) && __builtin_isfinite(ay) && __builtin_isfinite(az)), 0)) {
+    // a non-finite sum (some quotient was not exact, or an input not finite), a damping force of the wave outside the
+    // float32 quotient's exact range (force), or a mass outside its divisor range: redo the list with IEEE divisions
+    if (__builtin_expect(force || !divisor_ok(mf) ||
+                         !(__builtin_isfinite(ax) && __builtin_isfinite(ay) && __builtin_isfinite(az)), 0)) {
         ax = 0.f; ay = 0.f; az = 0.f;
         for (int r = s0; r < s1; r++) {
             const int ent = inc[r];
@@ -717,13 +752,13 @@ __device__ __forceinline__ void mass_step(const KParams &kp, const double *st, c
                                           const uint16_t *inc, int lb, int s0, int s1, float mf,
                                           const float *p3, const float *v3, float &px, float &py, float &pz,
                                           float &vx, float &vy, float &vz, float &ax, float &ay, float &az,
-                                          bool &hit, int spring_mode, bool pinned) {
+                                          bool &hit, int spring_mode, bool pinned, bool force) {
     if (spring_mode == 2) {
         g3_mass_step(kp, st, inc, lb, s0, s1, mf, p3, v3, px, py, pz, vx, vy, vz, ax, ay, az, hit, pinned);
         return;
     }
     mass_accumulate(TermsAoS{const_cast<double *>(st), const_cast<float *>(sdf)}, inc, lb, s0, s1, mf, ax, ay, az,
-                    spring_mode);
+                    spring_mode, force);
     const float ymf = (float)(1.0 / (double)mf);
     mass_tail(kp, mf, ymf, p3, v3, px, py, pz, vx, vy, vz, ax, ay, az, hit, pinned);
 }
@@ -971,9 +1006,10 @@ __device__ __forceinline__ void g2_gravity_cold(double cgd, float d0, float d1, 
     q2 = ((f * d2) / dv) / mf;
 }
 // RN32(a / b) for a float32 a and b from y ~ 1/b (rcp64_nr, within ~1 ulp of a double): the double product a * y lies
-// within 2^-51 (relative) of a / b, and a quotient of two 24-bit floats is at least 2^-47 from every float32 rounding
-// midpoint (subnormal results included), so the one rounding to float32 is RN32(a / b); zero, inf and NaN
-// numerators propagate as IEEE division does.  b must be finite, nonzero and normal (the callers' guards).
+// within 2^-51 (relative) of a / b, and a quotient of two 24-bit floats that is a normal float32 is at least 2^-47
+// from every float32 rounding midpoint, so the one rounding to float32 is RN32(a / b); zero, inf and NaN numerators
+// propagate as IEEE division does.  A subnormal quotient can sit ON a midpoint (x / 6 for x = odd * 3 * 2^-149): the
+// callers keep the operands in the exact range (TINY_EXP), which keeps every quotient normal.
 __device__ __forceinline__ float fdiv_rcp(float a, double y) { return (float)((double)a * y); }
 // G2 gravity_vec partner, fast form: np_norm3's sum, sqrt_mid, numpy's distance ** 2 (np_sq: RN(x*x) or, for the
 // 0.29 % of distances near a rounding boundary, the restated powf), the four quotients by fdiv_rcp from two
@@ -984,20 +1020,23 @@ __device__ __forceinline__ void g2_gravity_fast(float cg, float d0, float d1, fl
                                                 float &q1, float &q2, bool &ok) {
     const float sq = (float)(((double)(d0 * d0) + (double)(d1 * d1)) + (double)(d2 * d2));
     const float dist = sqrt_mid(sq);
-    ok = sq >= 0x1p-96f && sq < 0x1p126f;
     const float dd = np_sq(dist);
     const float f = fdiv_rcp(cg, rcp64_nr((double)dd));
     const double yd = rcp64_nr((double)dist);
-    q0 = fdiv_exact(fdiv_rcp(f * d0, yd), ym);
-    q1 = fdiv_exact(fdiv_rcp(f * d1, yd), ym);
-    q2 = fdiv_exact(fdiv_rcp(f * d2, yd), ym);
+    const float e0 = f * d0, e1 = f * d1, e2 = f * d2;
+    // the exact range: distance in [2^-20, 2^20) (inside sqrt_mid's range), the dividends cg and f * d either 0 or at
+    // least 2^-80: every quotient (cg / dd, e / dist, then / m with m in its divisor range) is then a normal float32
+    ok = sq >= 0x1p-40f && sq < 0x1p40f && min(fexp(cg), fexp3(e0, e1, e2)) >= TINY_EXP;
+    q0 = fdiv_exact(fdiv_rcp(e0, yd), ym);
+    q1 = fdiv_exact(fdiv_rcp(e1, yd), ym);
+    q2 = fdiv_exact(fdiv_rcp(e2, yd), ym);
 }
 __device__ __forceinline__ void g2_gravity_term(double cgd, float d0, float d1, float d2, float mf, double ym,
                                                 float &ax, float &ay, float &az) {
     float q0, q1, q2;
     bool ok = WG_FAST_PAIR;
     if (WG_FAST_PAIR) g2_gravity_fast((float)cgd, d0, d1, d2, ym, q0, q1, q2, ok);
-    if (__builtin_expect(!ok, 0)) g2_gravity_cold(cgd, d0, d1, d2, mf, q0, q1, q2);
+    if (__builtin_expect(!ok || !divisor_ok(mf), 0)) g2_gravity_cold(cgd, d0, d1, d2, mf, q0, q1, q2);
     ax = ax + q0;
     ay = ay + q1;
     az = az + q2;
@@ -1253,6 +1292,7 @@ __global__ __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(wg_kernel_
     if (STEP) {
         // ================= 2. edge phase =================
         // spring (gym/engine.py:78-102) + damping (gym/optimized_walker.py:92-106)
+        bool gtiny = false;
         for (int pass = 0; pass * EPL * T < nE; pass++) {
 #pragma unroll
             for (int it = 0; it < EPL; it++) {
@@ -1272,10 +1312,12 @@ __global__ __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(wg_kernel_
                     const int wl = fdiv(le, b.K, geo.invK);
                     lm = wl * b.M; ew = le - wl * b.K; Aw = b.A; ub = wl * b.A;
                 }
-                spring_edge(e, le, lm, (ew < Aw) ? s.x[ub + ew] : e.rest, s.pos, s.vel, s.t, s.df, kp.spring_mode);
+                spring_edge(e, le, lm, (ew < Aw) ? s.x[ub + ew] : e.rest, s.pos, s.vel, s.t, s.df, kp.spring_mode,
+                            gtiny);
             }
         }
-        __syncthreads();
+        // any damping force of the tile outside the exact range of the mass loop's float32 quotient: IEEE divisions
+        const bool tiny_blk = __syncthreads_or(gtiny) != 0;
 
         // ================= 3. mass phase: ordered accumulation, env forces, run1 =================
         const uint16_t *s_inc16 = reinterpret_cast<const uint16_t *>(s.inc);
@@ -1301,7 +1343,7 @@ __global__ __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(wg_kernel_
                 const int lb = RAGGED ? s.eoff[wl] : wl * b.K;
                 const int M = RAGGED ? s.moff[wl + 1] - lm : b.M;
                 const float mf = s.m[lp];
-                mass_accumulate(TermsAoS{s.t, s.df}, s_inc16 + 2 * lb, lb, s0, s1, mf, ax, ay, az, 0);
+                mass_accumulate(TermsAoS{s.t, s.df}, s_inc16 + 2 * lb, lb, s0, s1, mf, ax, ay, az, 0, tiny_blk);
                 pair_forces_lds(b, kp, s.pos, s.m, lm, M, lp - lm, (size_t)P0 + lm, mf, ax, ay, az);
                 s.acc[3 * lp] = ax; s.acc[3 * lp + 1] = ay; s.acc[3 * lp + 2] = az;
             }
@@ -1321,7 +1363,7 @@ __global__ __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(wg_kernel_
             } else {
                 mass_step(kp, s.t, s.df, s_inc16 + 2 * lb, lb, s0, (WG_ABLATE & 2) ? min(s1, s0 + 1) : s1, mf,
                           s.pos + 3 * lp, s.vel + 3 * lp, px, py, pz, vx, vy, vz, ax, ay, az, hit, kp.spring_mode,
-                          b.pinned && b.pinned[P0 + lp]);
+                          b.pinned && b.pinned[P0 + lp], tiny_blk);
             }
             if (b.contact) b.contact[P0 + lp] = (uint8_t)hit;
             if (b.radius) b.radius[P0 + lp] = hit ? 3.0 : 1.0;   // gym/optimized_env.py:156,175
@@ -1602,16 +1644,20 @@ __device__ __forceinline__ void spring_terms_cold(const EdgeRec &e, float x, flo
 }
 
 
+// pos_ok (wave-uniform): every position component of the wave's masses is 0 or at least 2^-56 in magnitude, so every
+// difference r is 0 or at least 2^-79 (a multiple of 2^-79, the spacing of floats at 2^-56) and the d quotients' dividends
+// are in the exact range without a test per spring
 __device__ __forceinline__ void spring_terms(const EdgeRec &e, float x, float pix, float piy, float piz, float pjx,
                                              float pjy, float pjz, float vix, float viy, float viz, float vjx,
                                              float vjy, float vjz, double &t0, double &t1, double &t2, float &g0,
-                                             float &g1, float &g2, int spring_mode) {
+                                             float &g1, float &g2, int spring_mode, bool pos_ok) {
     const float r0 = pjx - pix, r1 = pjy - piy, r2 = pjz - piz;     // other.pos - self.pos
     float d0, d1, d2;
 #if WG_FAST_SPRING
     // np.linalg.norm(p_i - p_j) (engine.py:86): squares summed in float64, rounded, sqrt.  (p_i - p_j)^2 == r^2.
     const float sq = (float)(((double)(r0 * r0) + (double)(r1 * r1)) + (double)(r2 * r2));
-    const bool mid = sq >= 0x1p-96f && sq < 0x1p126f;                // false for NaN
+    // sqrt_mid's range is [2^-96, 2^126); the d quotients' exact range asks cur in [2^-20, 2^20) (false for NaN)
+    const bool mid = sq >= 0x1p-40f && sq < 0x1p40f;
     const float cur = sqrt_mid(sq);
     const float dx = cur - x;                                       // engine.py:96
     // cur >= 2^-48 > Config.r: max(distance, r) is the distance itself
@@ -1630,7 +1676,9 @@ __device__ __forceinline__ void spring_terms(const EdgeRec &e, float x, float pi
     }
     // the quotients are exact when every one is finite; a non-finite one makes its sum non-finite (|d| <= 1
     // cannot overflow a sum of three)
-    const bool fast_ok = mid && __builtin_isfinite(d0 + d1 + d2) && __builtin_isfinite(t0 + t1 + t2);
+    bool rok = true;
+    if (__builtin_expect(!pos_ok, 0)) rok = fexp3(r0, r1, r2) >= TINY_EXP;
+    const bool fast_ok = mid && rok && __builtin_isfinite(d0 + d1 + d2) && __builtin_isfinite(t0 + t1 + t2);
     if (__builtin_expect(!fast_ok, 0)) spring_terms_cold(e, x, r0, r1, r2, t0, t1, t2, d0, d1, d2, spring_mode);
 #else
     spring_terms_cold(e, x, r0, r1, r2, t0, t1, t2, d0, d1, d2, spring_mode);
@@ -1639,14 +1687,19 @@ __device__ __forceinline__ void spring_terms(const EdgeRec &e, float x, float pi
     const float dkc = dk * e.c;                                               // :104
     g0 = dkc * d0; g1 = dkc * d1; g2 = dkc * d2;
 }
+// gt: a damping-force component below the exact range of the mass loop's float32 quotient (the wave then runs its mass
+// loop with IEEE divisions)
 template <class TS>
 __device__ __forceinline__ void spring_edge_regs(const EdgeRec &e, int le, float x, float pix, float piy, float piz,
                                                  float pjx, float pjy, float pjz, float vix, float viy, float viz,
-                                                 float vjx, float vjy, float vjz, const TS &ts, int spring_mode) {
+                                                 float vjx, float vjy, float vjz, const TS &ts, int spring_mode, bool &gt,
+                                                 bool pos_ok) {
     double t0, t1, t2;
     float g0, g1, g2;
-    spring_terms(e, x, pix, piy, piz, pjx, pjy, pjz, vix, viy, viz, vjx, vjy, vjz, t0, t1, t2, g0, g1, g2, spring_mode);
+    spring_terms(e, x, pix, piy, piz, pjx, pjy, pjz, vix, viy, viz, vjx, vjy, vjz, t0, t1, t2, g0, g1, g2, spring_mode,
+                 pos_ok);
     ts.put(le, t0, t1, t2, g0, g1, g2);
+    gt = gt || fexp3(g0, g1, g2) < TINY_EXP;
 }
 
 // ------------------------------------------------------------------ lean wave tile: loads, then compute
@@ -1971,6 +2024,8 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
     STAMP(2);
 
     // ================= springs: gym/engine.py:78-102 + gym/optimized_walker.py:92-106 =================
+    bool gtiny = false;   // a damping force of this lane's springs outside the mass loop's exact quotient range
+    const bool pos_ok = __all(fexp3(L.p3[0], L.p3[1], L.p3[2]) >= -55);   // (spring_terms)
     // endpoint state from the mass lanes by ds_bpermute: every lane takes part (inactive sources read as 0).
     // (Issuing pass it + 1's gathers before pass it's arithmetic needs 90 VGPRs, 5 waves per SIMD: 48.5 against
     // 47.8 us per launch, profiles/r02_ab_spring_pipe.json.)
@@ -2001,7 +2056,7 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
                        g.v[2] + g.v[5] + g.v[8] + g.v[11], e.k, e.c, 0.f);
             } else {
                 spring_edge_regs(e, le, xr, g.v[0], g.v[1], g.v[2], g.v[3], g.v[4], g.v[5], g.v[6], g.v[7], g.v[8],
-                                 g.v[9], g.v[10], g.v[11], ts, 0);   // lean path: spring_mode 0 only
+                                 g.v[9], g.v[10], g.v[11], ts, 0, gtiny, pos_ok);   // lean path: spring_mode 0 only
             }
         }
     };
@@ -2015,6 +2070,9 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
         spring(it, g);
     }
     wave_sync();
+    // any spring of the wave with a damping force outside the exact range: every mass loop of the wave divides by m with
+    // IEEE divisions (rare: damping forces below 2^-80)
+    const bool wave_tiny = __any(gtiny);
     STAMP(3);
 
     // ================= masses: ordered accumulation, env forces, Point.run1 =================
@@ -2026,10 +2084,11 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
         const int lb = wl * K;
         // (the resident kernel keeps the XOR sign form: 5 fewer registers where its carried state is live)
         if (WG_MASS_V2 && !RES)
-            mass_accumulate_v2(ts, reinterpret_cast<const uint16_t *>(s_inc) + 2 * lb, lb, L.io0, r1, mf, ym, ax, ay, az);
+            mass_accumulate_v2(ts, reinterpret_cast<const uint16_t *>(s_inc) + 2 * lb, lb, L.io0, r1, mf, ym, ax, ay, az,
+                               wave_tiny);
         else
             mass_accumulate<LeanTerms, !RES>(ts, reinterpret_cast<const uint16_t *>(s_inc) + 2 * lb, lb, L.io0, r1, mf,
-                                             ax, ay, az, 0);
+                                             ax, ay, az, 0, wave_tiny);
     }
     // every lane (gathers); the resident kernel runs pair-free batches only (wg_rollout falls back to wg_step)
     if (!RES && kp.pair_mode) pair_forces(b, kp, L.p3, mf, pl, lane, M, is_mass, ax, ay, az);
@@ -2165,7 +2224,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lean_waves(
 // walker_step_lean, step for step (bit-identical to n_steps single-step launches).
 template <bool IN3D, int NE>
 #ifndef WG_RES_WAVES
-#define WG_RES_WAVES 5   // waves per SIMD the resident kernel's register budget targets (its state stays live)
+#define WG_RES_WAVES 4   // waves per SIMD the resident kernel's register budget targets (its state stays live)
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4 : WG_RES_WAVES))) void walker_rollout_lean(
     wg_batch b, KParams kp, const float *__restrict__ action, int action_cols, int action_stride, int64_t action_step,
@@ -2376,6 +2435,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
     STAMP(2);
 
     // ================= springs: gym/engine.py:78-102 + gym/optimized_walker.py:92-106 =================
+    bool gtiny = false;   // a damping force of this lane's springs outside the mass loop's exact quotient range
+    const bool pos_ok = __all(fexp3(p3[0], p3[1], p3[2]) >= -55);   // (spring_terms)
 #pragma unroll
     for (int it = 0; it < NE; it++) {
         if (64 * it >= nE) continue;                       // wave-uniform
@@ -2392,9 +2453,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
         const float xs = s_x[mus ? s_uo[ew_w] + ew : 0];
         const float xr = mus ? xs : e.rest;
         if (le < nE)
-            spring_edge_regs(e, le, xr, pix, piy, piz, pjx, pjy, pjz, vix, viy, viz, vjx, vjy, vjz, ts, 0);
+            spring_edge_regs(e, le, xr, pix, piy, piz, pjx, pjy, pjz, vix, viy, viz, vjx, vjy, vjz, ts, 0, gtiny, pos_ok);
     }
     wave_sync();
+    // any spring of the wave with a damping force outside the exact range: every mass loop of the wave divides by m with
+    // IEEE divisions (rare: damping forces below 2^-80)
+    const bool wave_tiny = __any(gtiny);
     STAMP(3);
 
     // ================= masses: ordered accumulation, env forces, Point.run1 =================
@@ -2402,10 +2466,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
     bool hit = false;
     if (is_mass) {
         if (WG_MASS_V2)
-            mass_accumulate_v2(ts, reinterpret_cast<const uint16_t *>(s_inc) + 2 * mlb, mlb, io0, io1, mf, ym, ax, ay, az);
+            mass_accumulate_v2(ts, reinterpret_cast<const uint16_t *>(s_inc) + 2 * mlb, mlb, io0, io1, mf, ym, ax, ay, az,
+                               wave_tiny);
         else
             mass_accumulate<TermsAoS, true>(ts, reinterpret_cast<const uint16_t *>(s_inc) + 2 * mlb, mlb, io0, io1, mf,
-                                            ax, ay, az, 0);
+                                            ax, ay, az, 0, wave_tiny);
         mass_tail(kp, mf, (float)ym, p3, v3, px, py, pz, vx, vy, vz, ax, ay, az, hit, pin != 0);
         const uint32_t pl = (uint32_t)(P0 + lane);
         float *gpo = b.pos + 3 * (size_t)pl, *gvo = b.vel + 3 * (size_t)pl, *gao = b.acc + 3 * (size_t)pl;

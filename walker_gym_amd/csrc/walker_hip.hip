@@ -247,6 +247,9 @@ __device__ inline float fdiv_exact(float x, double y) { return (float)((double)x
 // double product rounded to a subnormal float can sit on a rounding midpoint.  fexp is frexp's exponent (0 for 0,
 // inf and NaN: zero dividends pass), so one min over fexp's tests a whole set of dividends.
 constexpr int TINY_EXP = -79;   // fexp(x) >= TINY_EXP  <=>  x == 0 or |x| >= 2^-80
+#ifndef WG_GUARDS
+#define WG_GUARDS 15   // diagnostic builds only (cost A/B, results not exact): bit 1 spring dividends, 2 damping
+#endif                 // forces, 4 env dividends, 8 mass range; the product keeps all four
 __device__ __forceinline__ int fexp(float x) { return __builtin_amdgcn_frexp_expf(x); }
 __device__ __forceinline__ int fexp3(float a, float b, float c) { return min(min(fexp(a), fexp(b)), fexp(c)); }
 __device__ __forceinline__ bool divisor_ok(float m) {   // m in [2^-20, 2^21) in magnitude
@@ -533,7 +536,7 @@ __device__ __forceinline__ void mass_tail(const KParams &kp, float mf, float ymf
         int emin = 0;
         env_forces<true>(kp, mf, ymf, vx, vy, vz, py, ax, ay, az, hit, emin);
         // cold: redo with exact quotients (a non-finite sum, a dividend or the mass outside the exact range)
-        if (__builtin_expect(!__builtin_isfinite(ax + ay + az) || emin < TINY_EXP || !divisor_ok(mf), 0)) {
+        if (__builtin_expect(!__builtin_isfinite(ax + ay + az) || ((WG_GUARDS & 4) && (emin < TINY_EXP || !divisor_ok(mf))), 0)) {
             ax = sx; ay = sy; az = sz;
             env_forces<false>(kp, mf, ymf, vx, vy, vz, py, ax, ay, az, hit, emin);
         }
@@ -696,7 +699,7 @@ __device__ __forceinline__ void mass_accumulate_v2(const TermsAoS &ts, const uin
     }
     // a non-finite sum (some quotient was not exact, or an input not finite), a damping force of the wave outside the
     // float32 quotient's exact range (force), or a mass outside its divisor range: redo the list with IEEE divisions
-    if (__builtin_expect(force || !divisor_ok(mf) ||
+    if (__builtin_expect(force || ((WG_GUARDS & 8) && !divisor_ok(mf)) ||
                          !(__builtin_isfinite(ax) && __builtin_isfinite(ay) && __builtin_isfinite(az)), 0)) {
         ax = 0.f; ay = 0.f; az = 0.f;
         for (int r = s0; r < s1; r++) {
@@ -1677,7 +1680,7 @@ __device__ __forceinline__ void spring_terms(const EdgeRec &e, float x, float pi
     // the quotients are exact when every one is finite; a non-finite one makes its sum non-finite (|d| <= 1
     // cannot overflow a sum of three)
     bool rok = true;
-    if (__builtin_expect(!pos_ok, 0)) rok = fexp3(r0, r1, r2) >= TINY_EXP;
+    if ((WG_GUARDS & 1) && __builtin_expect(!pos_ok, 0)) rok = fexp3(r0, r1, r2) >= TINY_EXP;
     const bool fast_ok = mid && rok && __builtin_isfinite(d0 + d1 + d2) && __builtin_isfinite(t0 + t1 + t2);
     if (__builtin_expect(!fast_ok, 0)) spring_terms_cold(e, x, r0, r1, r2, t0, t1, t2, d0, d1, d2, spring_mode);
 #else
@@ -1699,7 +1702,7 @@ __device__ __forceinline__ void spring_edge_regs(const EdgeRec &e, int le, float
     spring_terms(e, x, pix, piy, piz, pjx, pjy, pjz, vix, viy, viz, vjx, vjy, vjz, t0, t1, t2, g0, g1, g2, spring_mode,
                  pos_ok);
     ts.put(le, t0, t1, t2, g0, g1, g2);
-    gt = gt || fexp3(g0, g1, g2) < TINY_EXP;
+    if (WG_GUARDS & 2) gt = gt || fexp3(g0, g1, g2) < TINY_EXP;
 }
 
 // ------------------------------------------------------------------ lean wave tile: loads, then compute

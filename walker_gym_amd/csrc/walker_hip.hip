@@ -203,6 +203,42 @@ __device__ inline float pw_leaf(const float *a, int n, int st) {
     const float res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
     return seq_sum_lds(res, a + i * st, n - i, st);
 }
+// both of one reduction lane's sums in one path: the sequential 0 + a[0] + a[sa] + ... (seq_sum_lds's order) and numpy's
+// pairwise sum of p (n <= 128, pw_leaf's order), interleaved so that neither waits on the other's LDS round trips or
+// add chain (the wave kernel's reduction lanes took the two as divergent paths, one after the other)
+__device__ inline void dual_sum_lds(const float *a, int sa, const float *p, int sp, int n, float &rs, float &rp) {
+    float s = 0.f;
+    int i = 0;
+    if (n < 8) {                                           // pairwise == sequential below 8 terms
+        float q = 0.f;
+        for (; i + 4 <= n; i += 4) {
+            const float x0 = a[i * sa], x1 = a[(i + 1) * sa], x2 = a[(i + 2) * sa], x3 = a[(i + 3) * sa];
+            const float y0 = p[i * sp], y1 = p[(i + 1) * sp], y2 = p[(i + 2) * sp], y3 = p[(i + 3) * sp];
+            s = (((s + x0) + x1) + x2) + x3;
+            q = (((q + y0) + y1) + y2) + y3;
+        }
+        for (; i < n; i++) { s += a[i * sa]; q += p[i * sp]; }
+        rs = s; rp = q;
+        return;
+    }
+    float r0 = p[0], r1 = p[sp], r2 = p[2 * sp], r3 = p[3 * sp];
+    float r4 = p[4 * sp], r5 = p[5 * sp], r6 = p[6 * sp], r7 = p[7 * sp];
+    for (; i < 8; i += 4) {
+        const float x0 = a[i * sa], x1 = a[(i + 1) * sa], x2 = a[(i + 2) * sa], x3 = a[(i + 3) * sa];
+        s = (((s + x0) + x1) + x2) + x3;
+    }
+    for (; i < n - (n % 8); i += 8) {
+        const float *q = p + i * sp, *b = a + i * sa;
+        const float x0 = b[0], x1 = b[sa], x2 = b[2 * sa], x3 = b[3 * sa];
+        const float x4 = b[4 * sa], x5 = b[5 * sa], x6 = b[6 * sa], x7 = b[7 * sa];
+        r0 += q[0]; r1 += q[sp]; r2 += q[2 * sp]; r3 += q[3 * sp];
+        r4 += q[4 * sp]; r5 += q[5 * sp]; r6 += q[6 * sp]; r7 += q[7 * sp];
+        s = (((((((s + x0) + x1) + x2) + x3) + x4) + x5) + x6) + x7;
+    }
+    float res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+    for (; i < n; i++) { s += a[i * sa]; res += p[i * sp]; }
+    rs = s; rp = res;
+}
 template <int D>
 __device__ inline float pw_tree(const float *a, int n, int st) {
     if (D == 0 || n <= 128) return pw_leaf(a, n, st);
@@ -247,6 +283,9 @@ __device__ inline float fdiv_exact(float x, double y) { return (float)((double)x
 // double product rounded to a subnormal float can sit on a rounding midpoint.  fexp is frexp's exponent (0 for 0,
 // inf and NaN: zero dividends pass), so one min over fexp's tests a whole set of dividends.
 constexpr int TINY_EXP = -79;   // fexp(x) >= TINY_EXP  <=>  x == 0 or |x| >= 2^-80
+#ifndef WG_DUAL_SUM
+#define WG_DUAL_SUM 1   // wave kernel: the reduction lanes' sequential and pairwise sums in one interleaved path
+#endif
 #ifndef WG_GUARDS
 #define WG_GUARDS 15   // diagnostic builds only (cost A/B, results not exact): bit 1 spring dividends, 2 damping
 #endif                 // forces, 4 env dividends, 8 mass range; the product keeps all four
@@ -2508,6 +2547,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
         if (r == 7) {
             const unsigned long long wm = (M == 64) ? ~0ull : (((1ull << M) - 1ull) << lm);
             v = __int_as_float((__popcll(hb & wm) << 1) | ((sb & wm) == wm ? 1 : 0));
+        } else if (WG_DUAL_SUM) {
+            // every lane runs both sums (one path): lanes 0-2 keep the sequential one, 3-6 the pairwise one
+            const float *src = r == 3 ? s_tp + 3 * lm + 1 : r == 5 ? s_tk + lm : r == 6 ? s_te + lm : s_tn + lm;
+            float vs, vp;
+            dual_sum_lds(s_tp + 3 * lm + (r < 3 ? r : 0), 3, src, r == 3 ? 3 : 1, M, vs, vp);
+            v = r < 3 ? vs : vp;
         } else if (r < 3) {
             v = seq_sum_lds(0.f, s_tp + 3 * lm + r, M, 3);
         } else {

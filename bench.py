@@ -229,6 +229,31 @@ def timed(env, acts, steps, lanes, stream):
 
 
 # ---------------------------------------------------------------- main
+def launch_floor(geo, stream, dev, n=2000):
+    """Per-launch time (us) of an empty kernel and of a one-load-one-store kernel on the step's grid, n launches back
+    to back on `stream` from one C call (wg_launch_floor, as wg_step issues a run's steps), beside a small batch's
+    step: the same box's latency floor."""
+    import ctypes as C
+    import torch
+    from walker_gym_amd import _lib
+    L = _lib.load()
+    blocks, threads = int(geo["blocks"]), int(geo["threads"])
+    src = torch.zeros(blocks * threads, device=dev)
+    dst = torch.empty_like(src)
+    args = (C.c_void_p(src.data_ptr()), C.c_void_p(dst.data_ptr()))
+    sp = C.c_void_p(stream.cuda_stream)
+    out = []
+    for mode in (0, 1):
+        _lib.check(L.wg_launch_floor(mode, blocks, threads, *args, 50, sp), "wg_launch_floor")
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        _lib.check(L.wg_launch_floor(mode, blocks, threads, *args, n, sp), "wg_launch_floor")
+        e1.record(stream)
+        torch.cuda.synchronize()
+        out.append(round(e0.elapsed_time(e1) / n * 1e3, 3))
+    return out
+
+
 def main():
     args = parse()
     ensure_world(args)
@@ -445,15 +470,18 @@ def main():
                                          "FP64_PEAK_TFS / FP32_PEAK_TFS, measured by scripts/valu_peak.hip)"),
                                 "hbm": {k: hbm[k] for k in ("achieved", "peak", "unit", "frac", "bytes_per_walker_step")}}
             line["pairs_per_s"] = round(pairs / (head_ms * 1e-3), 1)
-        floor_path = os.path.join(ROOT, "profiles", "r03_launch_floor.json")
-        if N <= 16384 and os.path.exists(floor_path):
-            # a small batch is one wave's latency chain per launch: state the launch floor it is bounded by
-            # (scripts/launch_floor.hip on a box: the same 128 x 256 geometry, back-to-back launches, HIP events)
-            fl = json.load(open(floor_path))
-            line["floor"] = {"empty_launch_us": fl["empty_us"], "load_store_launch_us": fl["load1_us"],
-                             "step_over_load_store": round(step_ms * 1e3 / fl["load1_us"], 3),
-                             "source": "profiles/r03_launch_floor.json (scripts/launch_floor.hip): back-to-back "
-                                       "launches of an empty kernel and of one coalesced load + store per lane"}
+        if N <= 16384:
+            # a small batch is one wave's latency chain per launch: state the launch floor it is bounded by, timed
+            # here, on this box and stream, for the step's own grid (wg_launch_floor: back-to-back launches of an
+            # empty kernel and of one coalesced load + store per thread, HIP events)
+            fl = launch_floor(geo, stream, dev)
+            line["floor"] = {"empty_launch_us": fl[0], "load_store_launch_us": fl[1],
+                             "step_over_load_store": round(step_ms * 1e3 / fl[1], 3),
+                             "kernel_over_load_store": round(head_ms * 1e3 / fl[1], 3),
+                             "grid": [geo["blocks"], geo["threads"]],
+                             "source": "wg_launch_floor on this box (the step's grid, 2,000 back-to-back launches "
+                                       "each, HIP events on the bench stream); scripts/launch_floor.hip is the "
+                                       "standalone form (profiles/r03_launch_floor.json)"}
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.workload, params, args.chain_points, args.cpu_seconds)
         print(json.dumps(line), flush=True)

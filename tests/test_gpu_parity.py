@@ -597,3 +597,25 @@ def test_kernel_variants_agree():
         for x, y in zip(lean, wg):
             assert x.shape == y.shape, name
             assert np.array_equal(x.view(np.uint8), y.view(np.uint8)), name
+
+
+def test_launch_floor_probe():
+    """wg_launch_floor (bench.py's same-box floor for small batches): mode 1 writes in + 1 over the whole grid, mode 0
+    touches nothing, and bad arguments are refused."""
+    import ctypes as C
+    import torch
+    from walker_gym_amd import _lib
+    L = _lib.load()
+    blocks, threads = 37, 256
+    src = torch.arange(blocks * threads, dtype=torch.float32, device="cuda:0")
+    dst = torch.full_like(src, -7.0)
+    sp = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    args = (C.c_void_p(src.data_ptr()), C.c_void_p(dst.data_ptr()))
+    assert L.wg_launch_floor(0, blocks, threads, *args, 3, sp) == 0
+    torch.cuda.synchronize()
+    assert (dst == -7.0).all()
+    assert L.wg_launch_floor(1, blocks, threads, *args, 2, sp) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(dst, src + 1)
+    assert L.wg_launch_floor(2, blocks, threads, *args, 1, sp) == _lib.WG_EINVAL
+    assert L.wg_launch_floor(1, blocks, 2048, *args, 1, sp) == _lib.WG_EINVAL

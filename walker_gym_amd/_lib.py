@@ -60,7 +60,7 @@ class WgLaunchInfo(C.Structure):
 
 
 EXPORTS = ("wg_abi_version", "wg_last_error", "wg_step", "wg_step_ranges", "wg_rollout", "wg_observe", "wg_reset", "wg_reset_noise",
-           "wg_plan_ragged", "wg_plan_waves", "wg_wave_edge_passes", "wg_plan_errors", "wg_launch_geometry")
+           "wg_plan_ragged", "wg_plan_waves", "wg_wave_edge_passes", "wg_plan_errors", "wg_launch_geometry", "wg_launch_floor")
 
 _lib = None
 _lock = threading.Lock()
@@ -97,8 +97,9 @@ def load(path: str | None = None):
         L.wg_wave_edge_passes.argtypes = [C.c_int32, C.c_int32]
         L.wg_plan_errors.argtypes = [C.c_int32]
         L.wg_launch_geometry.argtypes = [C.POINTER(WgBatch), C.POINTER(WgLaunchInfo)]
+        L.wg_launch_floor.argtypes = [C.c_int32, C.c_int32, C.c_int32, _vp, _vp, C.c_int32, _vp]
         for f in ("wg_step", "wg_step_ranges", "wg_rollout", "wg_observe", "wg_reset", "wg_reset_noise", "wg_plan_ragged", "wg_plan_waves",
-                  "wg_wave_edge_passes", "wg_plan_errors", "wg_launch_geometry"):
+                  "wg_wave_edge_passes", "wg_plan_errors", "wg_launch_geometry", "wg_launch_floor"):
             getattr(L, f).restype = C.c_int
         v = L.wg_abi_version()
         if v != ABI_VERSION:

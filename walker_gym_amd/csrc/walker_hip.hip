@@ -164,10 +164,20 @@ __device__ inline Carve carve(char *s, const Geo &g) {
 
 // ------------------------------------------------------------------ numpy-exact float helpers
 // np.linalg.norm of a float32 3-vector: OpenBLAS sdot (float products summed in double), float sqrt.
+// sqrtf of a float s in [2^-96, 2^126): v_sqrt_f32 and the one-ulp correction, the same steps as the compiler's
+// correctly rounded sqrtf minus its small-input rescaling and zero/inf fix-up, which this range never needs
+__device__ __forceinline__ float sqrt_mid(float s) {
+    const float r = __builtin_amdgcn_sqrtf(s);
+    const float rd = __uint_as_float(__float_as_uint(r) - 1u), ru = __uint_as_float(__float_as_uint(r) + 1u);
+    float o = (__builtin_fmaf(-rd, r, s) <= 0.f) ? rd : r;
+    return (__builtin_fmaf(-ru, r, s) > 0.f) ? ru : o;
+}
 __device__ inline float np_norm3(float x, float y, float z) {
     const float px = x * x, py = y * y, pz = z * z;
     double s = 0.0;
     s += (double)px; s += (double)py; s += (double)pz;
+    // (sqrt_mid where its range allows, the compiler's sqrtf elsewhere, ran 1 % slower: the branch costs more than
+    // the rescaling it skips, profiles/r03zm_ab_norm_*.txt)
     return sqrtf((float)s);
 }
 __device__ inline float np_dot3(float ax, float ay, float az, float bx, float by, float bz) {
@@ -364,14 +374,6 @@ __device__ __forceinline__ float fdiv_count(float x, float fM, double yM) {
     return q;
 }
 
-// sqrtf of a float s in [2^-96, 2^126): v_sqrt_f32 and the one-ulp correction, the same steps as the compiler's
-// correctly rounded sqrtf minus its small-input rescaling and zero/inf fix-up, which this range never needs
-__device__ __forceinline__ float sqrt_mid(float s) {
-    const float r = __builtin_amdgcn_sqrtf(s);
-    const float rd = __uint_as_float(__float_as_uint(r) - 1u), ru = __uint_as_float(__float_as_uint(r) + 1u);
-    float o = (__builtin_fmaf(-rd, r, s) <= 0.f) ? rd : r;
-    return (__builtin_fmaf(-ru, r, s) > 0.f) ? ru : o;
-}
 
 // numpy's float32 `x ** 2` (a scalar power: libm powf, not x*x; powf2.h): RN(x*x) unless x*x lies within 2^-32 of a
 // float rounding boundary (0.29 % of floats), then glibc's algorithm restated (cold, only the lanes that need it)
@@ -536,7 +538,9 @@ __device__ __forceinline__ float fdiv_env(float x, float m, float y) { return FA
 template <bool FAST>
 __device__ __forceinline__ void env_forces(const KParams &kp, float mf, float ymf, float vx, float vy, float vz,
                                            float py, float &ax, float &ay, float &az, bool &hit, int &emin) {
-    const float zm = fdiv_mk(0.f, mf, ymf);   // the zero components of the env forces, divided by m
+    // the zero components of the env forces, divided by m: FAST takes Markstein's unguarded step (exact 0/m for m in
+    // the divisor range, which the caller's test requires of the fast result; NaN for a tiny m, which it catches too)
+    const float zm = FAST ? fdiv_fast(0.f, mf, ymf) : fdiv_mk(0.f, mf, ymf);
     // gravity [0,-g,0]/m, damp -dampk*v/m  (gym/env.py:32-33, optimized_env.py:148-151)
     const float dvx = kp.neg_dampk * vx, dvy = kp.neg_dampk * vy, dvz = kp.neg_dampk * vz;
     if (FAST) {
@@ -3048,6 +3052,13 @@ int run(const wg_batch *b, const wg_params *p, const float *action, int32_t cols
     return 0;
 }
 
+// the launch floor beside a small step (bench.py): an empty launch, and one coalesced load + store per thread
+__global__ __launch_bounds__(1024) void floor_empty_kernel(float *) {}
+__global__ __launch_bounds__(1024) void floor_load_store_kernel(const float *__restrict__ in, float *__restrict__ out) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    out[i] = in[i] + 1.0f;
+}
+
 }  // namespace
 
 extern "C" {
@@ -3162,6 +3173,21 @@ int wg_plan_ragged(const int32_t *mass_off, const int32_t *edge_off, const int32
         plan[++blocks] = w;
     }
     return blocks;
+}
+
+// the launch floor beside a small step (bench.py)
+int wg_launch_floor(int32_t mode, int32_t blocks, int32_t threads, const float *in, float *out, int32_t n_launches,
+                    hipStream_t stream) {
+    if (blocks < 1 || threads < 1 || threads > 1024 || n_launches < 0 || (mode != 0 && mode != 1) ||
+        (mode == 1 && (!in || !out)))
+        return fail(WG_EINVAL, "bad floor launch (mode %d, %d x %d)", mode, blocks, threads);
+    for (int i = 0; i < n_launches; i++) {
+        if (mode == 0)
+            hipLaunchKernelGGL(floor_empty_kernel, dim3(blocks), dim3(threads), 0, stream, out);
+        else
+            hipLaunchKernelGGL(floor_load_store_kernel, dim3(blocks), dim3(threads), 0, stream, in, out);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : fail(WG_EHIP, "floor launch failed");
 }
 
 // diagnostic builds (-DWG_STAMPS): copy n lean-wave stamp records (8 x u64 each) to host memory; WG_EINVAL otherwise

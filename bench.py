@@ -13,8 +13,10 @@ with obs/reward/done/info materialised every step.  The batch is split into walk
 HIP streams (BatchedPhysicsEnv.run lanes: 2 for batches of >= 2^19 masses), one launch per range per step:
 every walker takes every step, and one range's next step fills the GPU while the other's drains.  Inputs
 (state, topology and a distinct U(-1,1) action tensor for every timed step) are resident in HBM before timing.
-Weak scaling: each rank owns its own `--walkers` walkers (no data-path collective); at rollout end the final
-observations are gathered with one RCCL all_gather_into_tensor (inside the timed region).
+Weak scaling: each rank owns its own `--walkers` walkers (no data-path collective); one rollout-end gather of a
+rollout's final observations (one RCCL all_gather_into_tensor) runs inside the timed region: by default this rollout's,
+after its last step (`--gather serial`), or the previous rollout's while this one steps (`--gather pipelined`,
+double-buffered as an actor loop would run it; slower on one MI355X).
 Rank 0 prints ONE JSON line.  Workloads: canonical (M=16, K=40, A=8; config 3/4),
 balance (Balance-v0; config 2 at --walkers 4096), ragged (M ~ U{4..32}; config 5), chain (performance_demo's
 chain of --chain-points masses with per-walker Point.gravity; §8(f) 3).
@@ -67,6 +69,10 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline samples")
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--gather", choices=["serial", "pipelined"], default="serial",
+                    help="rollout-end observation gather inside the timed region: serial (default: this rollout's "
+                         "final observations, after its last step) or pipelined (the previous rollout's, gathered "
+                         "while this rollout steps; measured slower on one MI355X: RCCL's kernels stall the steps)")
     ap.add_argument("--no-control", action="store_true", help="skip the single-launch (lanes 1) control timing")
     ap.add_argument("--dry-run", action="store_true", help="rank plumbing only (no GPU): every rank reports itself")
     return ap.parse_args(argv)
@@ -262,7 +268,7 @@ def main():
     import torch
     import torch.distributed as dist
     from walker_gym_amd.batched_env import BatchedPhysicsEnv
-    from walker_gym_amd.distributed import gather_rollout
+    from walker_gym_amd.distributed import gather_rollout, gather_rollout_async
     from walker_gym_amd.layout import layout_bytes_per_walker_step
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -314,17 +320,27 @@ def main():
         init_group()
     if in_world:
         dist.barrier()
+    do_gather = in_world and not args.no_gather
+    # pipelined gather: the send buffer holds the previous rollout's final observations (here the warm-up's)
+    prev_obs = env.obs.clone() if do_gather and args.gather == "pipelined" else None
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
+    pending = None
+    if prev_obs is not None:
+        # issued before the steps: RCCL runs it on its own stream while the walker ranges step
+        pending = gather_rollout_async(prev_obs, n_total=world * N)
     if graph is not None:
         graph.replay()
     else:
         env.run(acts, args.steps, lanes=lanes)
     ev1.record(stream)
     gathered = None
-    if in_world and not args.no_gather:
+    if pending is not None:
+        next_obs = env.obs.clone()     # this rollout's final observations: the next rollout's send buffer
+        gathered = pending.wait()
+    elif do_gather:
         # rollout-end observation gather (RCCL all_gather_into_tensor), shard sizes from shard_bounds
         gathered = gather_rollout(env.obs, n_total=world * N)
     torch.cuda.synchronize()
@@ -338,6 +354,22 @@ def main():
     if in_world:
         dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
     wall_max = float(wall_t.item())
+    gather_info = None
+    if do_gather:
+        # one standalone gather, every rank, timed after the timed region: what the serial form adds per rollout
+        dist.barrier()
+        torch.cuda.synchronize()
+        tg = time.perf_counter()
+        gather_rollout(env.obs, n_total=world * N)
+        torch.cuda.synchronize()
+        tg_t = torch.tensor([time.perf_counter() - tg], dtype=torch.float64, device=dev)
+        dist.all_reduce(tg_t, op=dist.ReduceOp.MAX)
+        gather_info = {"mode": args.gather, "rows": world * N, "bytes_per_rank": int(env.obs.numel() * 4),
+                       "gathered_bytes": int(gathered.numel() * gathered.element_size()),
+                       "standalone_ms": round(float(tg_t.item()) * 1e3, 4),
+                       "note": "pipelined: the previous rollout's final observations gathered while this rollout "
+                               "steps (one full gather inside the timed region, overlapped); serial: this rollout's, "
+                               "after its last step; standalone_ms: one gather alone (max over ranks)"}
 
     if rank == 0:
         # single-launch control: one full-batch launch per step, HIP events on its stream — the per-dispatch
@@ -406,7 +438,7 @@ def main():
                                    f"({lanes} range{'s' if lanes > 1 else ''} on {lanes} stream{'s' if lanes > 1 else ''})"
                                    + (", replayed as one HIP graph" if graph is not None else ""),
                        "walkers_per_gpu": N, "total_walkers": world * N, "M": M, "K": K, "A": env.batch.A,
-                       "obs_dim": D, "parallelism": f"dp{world}", "rollout_gather": gathered is not None,
+                       "obs_dim": D, "parallelism": f"dp{world}", "rollout_gather": (args.gather if gathered is not None else False),
                        "dist_backend": (dist.get_backend() if in_world else None),
                        **({"dist_init": "before the env" if dist_first else "after the env's streams and warm-up"}
                           if in_world else {}),
@@ -482,6 +514,8 @@ def main():
                              "source": "wg_launch_floor on this box (the step's grid, 2,000 back-to-back launches "
                                        "each, HIP events on the bench stream); scripts/launch_floor.hip is the "
                                        "standalone form (profiles/r03_launch_floor.json)"}
+        if gather_info is not None:
+            line["gather"] = gather_info
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.workload, params, args.chain_points, args.cpu_seconds)
         print(json.dumps(line), flush=True)

@@ -21,11 +21,11 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n_total, T, out_q, by_size):
+def _worker(rank, world, port, n_total, T, out_q, by_size, pipelined=False):
     import torch
     import torch.distributed as dist
     from oracle.oracle import Oracle
-    from walker_gym_amd.distributed import gather_rollout
+    from walker_gym_amd.distributed import gather_rollout, gather_rollout_async
     from walker_gym_amd.synthetic import canonical_walkers
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -37,7 +37,15 @@ def _worker(rank, world, port, n_total, T, out_q, by_size):
     obs = None
     for t in range(T):
         obs = orc.step(acts[t, a:b])["obs"]
-    full = gather_rollout(torch.from_numpy(obs), n_total=None if by_size else n_total)
+    if pipelined:
+        # bench.py's pipelined gather: issue the gather of this rollout's final observations, keep stepping (the next
+        # rollout; the oracle writes fresh arrays, so the gathered buffer is not touched), then wait
+        h = gather_rollout_async(torch.from_numpy(obs.copy()), n_total=None if by_size else n_total)
+        for t in range(2):
+            orc.step(acts[t, a:b])
+        full = h.wait()
+    else:
+        full = gather_rollout(torch.from_numpy(obs), n_total=None if by_size else n_total)
     if rank == 0:
         out_q.put(full.numpy())
     dist.barrier()
@@ -53,16 +61,19 @@ def test_shard_bounds_cover():
             assert max(b - a for a, b in rs) - min(b - a for a, b in rs) <= 1
 
 
-@pytest.mark.parametrize("world,n_total,by_size", [(2, 64, False), (2, 65, False), (3, 65, True)])
-def test_gloo_matches_single_process(world, n_total, by_size):
-    """Even and uneven shards (65 walkers: ranks of 33/32 or 22/22/21), lengths from shard_bounds or gathered."""
+@pytest.mark.parametrize("world,n_total,by_size,pipelined", [(2, 64, False, False), (2, 65, False, False),
+                                                             (3, 65, True, False), (2, 65, False, True)])
+def test_gloo_matches_single_process(world, n_total, by_size, pipelined):
+    """Even and uneven shards (65 walkers: ranks of 33/32 or 22/22/21), lengths from shard_bounds or gathered; the
+    pipelined form (gather issued, more steps, then waited) gathers the same rows."""
     from oracle.oracle import Oracle
     from walker_gym_amd.synthetic import canonical_walkers
     T = 5
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n_total, T, q, by_size)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_total, T, q, by_size, pipelined))
+             for r in range(world)]
     for p in procs:
         p.start()
     got = q.get(timeout=180)

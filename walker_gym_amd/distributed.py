@@ -4,7 +4,8 @@ Walkers are independent (no inter-walker force on the env path), so a node-wide 
 contiguous walker blocks, one per rank (one process per GPU, torch.distributed over RCCL/xGMI).
 Stepping needs no communication at all; the only collective is the observation gather at the end
 of a rollout (``gather_rollout``: one all_gather_into_tensor on RCCL, all_gather on gloo; uneven
-shards are padded to the longest and trimmed).
+shards are padded to the longest and trimmed).  ``gather_rollout_async`` issues it without waiting, so
+an actor loop overlaps the gather of rollout i with the steps of rollout i + 1 (bench.py's default).
 Results of shard g are bit-identical to the same walkers stepped on one GPU (tested).
 """
 from __future__ import annotations
@@ -46,14 +47,34 @@ def shard_spec(spec: dict, start: int, stop: int) -> dict:
     return out
 
 
-def gather_rollout(local: torch.Tensor, group: Optional[dist.ProcessGroup] = None,
-                   n_total: Optional[int] = None) -> torch.Tensor:
-    """Concatenate every rank's [n_r, ...] block along dim 0, in rank order — the rollout-end gather.
+class GatherHandle:
+    """An issued rollout-end gather (gather_rollout_async): wait() makes the calling stream wait for the collective
+    and returns the gathered [n_total, ...] tensor.  The buffers stay referenced until then."""
 
-    Blocks may differ in length (shard_bounds gives the first n_total % world ranks one walker more): each
-    block is padded to the longest, gathered with one collective (all_gather_into_tensor on RCCL, all_gather
-    on gloo) and trimmed.  The lengths come from shard_bounds when ``n_total`` is given, otherwise from a
-    small all_gather of every rank's length."""
+    def __init__(self, work, out, sizes, nmax, world):
+        self._work, self._out, self._sizes, self._nmax, self._world = work, out, sizes, nmax, world
+
+    def wait(self) -> torch.Tensor:
+        if self._work is not None:
+            self._work.wait()
+            self._work = None
+        out, sizes, nmax = self._out, self._sizes, self._nmax
+        if all(sz == nmax for sz in sizes):
+            return out
+        return torch.cat([out[r * nmax:r * nmax + sizes[r]] for r in range(self._world)], 0)
+
+
+def gather_rollout_async(local: torch.Tensor, group: Optional[dist.ProcessGroup] = None,
+                         n_total: Optional[int] = None) -> GatherHandle:
+    """Issue the rollout-end gather (every rank's [n_r, ...] block concatenated along dim 0 in rank order) without
+    waiting for it: on RCCL the collective runs on the process group's own stream, ordered after the work already
+    queued on the calling stream, so steps issued afterwards overlap it (an actor loop gathers rollout i while
+    stepping rollout i + 1).  `local` must not be written until wait().
+
+    Blocks may differ in length (shard_bounds gives the first n_total % world ranks one walker more): each block is
+    padded to the longest, gathered with one collective (all_gather_into_tensor on RCCL, all_gather on gloo) and
+    trimmed.  The lengths come from shard_bounds when ``n_total`` is given, otherwise from a small (synchronous)
+    all_gather of every rank's length."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     n = int(local.shape[0])
@@ -72,9 +93,16 @@ def gather_rollout(local: torch.Tensor, group: Optional[dist.ProcessGroup] = Non
         block = torch.cat([block, block.new_zeros((nmax - n,) + tuple(local.shape[1:]))], 0)
     out = torch.empty((world * nmax,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
     if dist.get_backend(group) == "nccl":
-        dist.all_gather_into_tensor(out, block, group=group)
+        work = dist.all_gather_into_tensor(out, block, group=group, async_op=True)
     else:
-        dist.all_gather(list(out.chunk(world, 0)), block, group=group)
-    if all(sz == nmax for sz in sizes):
-        return out
-    return torch.cat([out[r * nmax:r * nmax + sizes[r]] for r in range(world)], 0)
+        work = dist.all_gather(list(out.chunk(world, 0)), block, group=group, async_op=True)
+    h = GatherHandle(work, out, sizes, nmax, world)
+    h._block = block   # (the padded copy, if any, lives until wait)
+    return h
+
+
+def gather_rollout(local: torch.Tensor, group: Optional[dist.ProcessGroup] = None,
+                   n_total: Optional[int] = None) -> torch.Tensor:
+    """Concatenate every rank's [n_r, ...] block along dim 0, in rank order — the rollout-end gather
+    (gather_rollout_async, waited for at once)."""
+    return gather_rollout_async(local, group, n_total).wait()

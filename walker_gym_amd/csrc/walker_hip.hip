@@ -378,9 +378,13 @@ __device__ __forceinline__ float fdiv_count(float x, float fM, double yM) {
 // numpy's float32 `x ** 2` (a scalar power: libm powf, not x*x; powf2.h): RN(x*x) unless x*x lies within 2^-32 of a
 // float rounding boundary (0.29 % of floats), then glibc's algorithm restated (cold, only the lanes that need it)
 __device__ __attribute__((noinline)) float np_sq_cold(float x) { return pw_pow2(x); }
+// INL: the restated powf inline instead of a call — the latency-bound small-tile instances (lean NE = 1: a launch lasts
+// as long as its slowest wave, and ~10 % of waves take this path): Balance-4096 -1.6 %, while the large tiles keep the
+// call (canonical +1.0 % inline; profiles/r03zq_ab_sqinl_*.txt)
+template <bool INL = false>
 __device__ __forceinline__ float np_sq(float x) {
     float f;
-    if (__builtin_expect(!pw_pow2_fast(x, &f), 0)) f = np_sq_cold(x);
+    if (__builtin_expect(!pw_pow2_fast(x, &f), 0)) f = INL ? pw_pow2(x) : np_sq_cold(x);
     return f;
 }
 
@@ -2142,7 +2146,7 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
         mass_tail(kp, mf, (float)ym, L.p3, L.v3, px, py, pz, vx, vy, vz, ax, ay, az, hit, pin);
         if (b.radius && store) b.radius[pl] = hit ? 3.0 : 1.0;   // p.r = 3 / p.r = 1 (gym/optimized_env.py:156,175)
         nv = np_norm3(vx, vy, vz);
-        ke = mf * np_sq(nv);   // p.m * norm(p.v) ** 2 (gym/optimized_env.py:242)
+        ke = mf * np_sq<NE == 1>(nv);   // p.m * norm(p.v) ** 2 (gym/optimized_env.py:242)
         pe = (float)((double)mf * kp.g) * (py - kp.ground);
     }
     STAMP(4);

@@ -323,6 +323,14 @@ def main():
     do_gather = in_world and not args.no_gather
     # pipelined gather: the send buffer holds the previous rollout's final observations (here the warm-up's)
     prev_obs = env.obs.clone() if do_gather and args.gather == "pipelined" else None
+    # the rollout SURVEY §8(e) gathers: every step's reward and done flags (written by the steps at per-step offsets,
+    # the same bytes as overwriting one row) and the final observations
+    rec = None
+    if do_gather and graph is None and prev_obs is None:
+        rec = {"reward": torch.empty((args.steps, N), dtype=torch.float32, device=dev),
+               "done": torch.empty((args.steps, N), dtype=torch.uint8, device=dev),
+               "energy": torch.empty((args.steps, N), dtype=torch.float32, device=dev),
+               "centroid": torch.empty((args.steps, N, 3), dtype=torch.float32, device=dev)}
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
@@ -334,15 +342,18 @@ def main():
     if graph is not None:
         graph.replay()
     else:
-        env.run(acts, args.steps, lanes=lanes)
+        env.run(acts, args.steps, lanes=lanes, record=rec)
     ev1.record(stream)
     gathered = None
     if pending is not None:
-        next_obs = env.obs.clone()     # this rollout's final observations: the next rollout's send buffer
-        gathered = pending.wait()
+        gathered = {"obs": pending.wait()}
     elif do_gather:
-        # rollout-end observation gather (RCCL all_gather_into_tensor), shard sizes from shard_bounds
-        gathered = gather_rollout(env.obs, n_total=world * N)
+        # rollout-end gather (RCCL all_gather_into_tensor, shard sizes from shard_bounds): the final observations
+        # [N, D] and, when recorded, every step's reward and done flags [K, N]
+        gathered = {"obs": gather_rollout(env.obs, n_total=world * N)}
+        if rec is not None:
+            gathered["reward"] = gather_rollout(rec["reward"], n_total=world * N, dim=1)
+            gathered["done"] = gather_rollout(rec["done"], n_total=world * N, dim=1)
     torch.cuda.synchronize()
     if in_world:
         dist.barrier()
@@ -361,43 +372,53 @@ def main():
         torch.cuda.synchronize()
         tg = time.perf_counter()
         gather_rollout(env.obs, n_total=world * N)
+        if rec is not None:
+            gather_rollout(rec["reward"], n_total=world * N, dim=1)
+            gather_rollout(rec["done"], n_total=world * N, dim=1)
         torch.cuda.synchronize()
         tg_t = torch.tensor([time.perf_counter() - tg], dtype=torch.float64, device=dev)
         dist.all_reduce(tg_t, op=dist.ReduceOp.MAX)
-        gather_info = {"mode": args.gather, "rows": world * N, "bytes_per_rank": int(env.obs.numel() * 4),
-                       "gathered_bytes": int(gathered.numel() * gathered.element_size()),
+        sent = {"obs": env.obs} if rec is None else {"obs": env.obs, "reward": rec["reward"], "done": rec["done"]}
+        gather_info = {"mode": args.gather, "rows": world * N, "tensors": sorted(gathered),
+                       "bytes_per_rank": int(sum(t.numel() * t.element_size() for t in sent.values())),
+                       "gathered_bytes": int(sum(t.numel() * t.element_size() for t in gathered.values())),
                        "standalone_ms": round(float(tg_t.item()) * 1e3, 4),
-                       "note": "pipelined: the previous rollout's final observations gathered while this rollout "
-                               "steps (one full gather inside the timed region, overlapped); serial: this rollout's, "
-                               "after its last step; standalone_ms: one gather alone (max over ranks)"}
+                       "note": "serial (default): this rollout's final observations [N, D] and its per-step reward "
+                               "and done flags [K, N], after its last step, inside the timed region; pipelined "
+                               "(opt-in): the previous rollout's final observations gathered while this rollout "
+                               "steps; standalone_ms: the same gathers alone (max over ranks)"}
 
     if rank == 0:
         # single-launch control: one full-batch launch per step, HIP events on its stream — the per-dispatch
         # duration a rocprofv3 kernel trace of `bench.py --lanes 1` reports (profiles/r02_*_kernel_stats*.csv)
-        n1 = max(20, min(args.steps, 200))
-        single_ms = step_ms if (lanes == 1 and graph is None) else None
+        # (200 launches with their own distinct actions whatever K is: at a short K the first launches of a process
+        # still see the clocks ramp, and the per-launch figure is the kernel's, not the bench's K)
+        n1 = 200
+        single_ms = step_ms if (lanes == 1 and graph is None and args.steps >= n1) else None
+        acts_c = acts[:n1] if args.steps >= n1 else \
+            (torch.rand((n1, N, A), generator=gen, device=dev) * 2 - 1).contiguous()
         if single_ms is None and not args.no_control:
-            env.run(acts[:n1], n1, lanes=1)
-            single_ms = timed(env, acts[:n1], n1, 1, stream)
+            env.run(acts_c, n1, lanes=1)
+            single_ms = timed(env, acts_c, n1, 1, stream)
         direct_ms = timed(env, acts, args.steps, lanes, stream) if graph is not None else None
         # closed loop: one BatchedPhysicsEnv.step per env step, as a policy loop calls it (the walker ranges join
         # at the end of every step, and every step returns obs/reward/done/info); the headline `value` instead
         # issues the K steps back to back (open loop: actions known up front, ranges drift out of phase)
         closed_ms = None
         if not args.no_control:
-            n_cl = max(20, min(args.steps, 200))
+            n_cl = n1
             for s_ in range(5):
-                env.step(acts[s_])
+                env.step(acts_c[s_])
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
             for s_ in range(n_cl):
-                env.step(acts[s_])
+                env.step(acts_c[s_])
             e1.record(stream)
             torch.cuda.synchronize()
             closed_ms = e0.elapsed_time(e1) / n_cl
         resident_ms = None
         if args.resident:
-            env.run(acts[:n1], n1, lanes=1, resident=True)
+            env.run(acts_c, n1, lanes=1, resident=True)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
             env.run(acts, args.steps, lanes=1, resident=True)
@@ -472,7 +493,7 @@ def main():
             line["closed_loop"] = {
                 "ms_per_step": round(closed_ms, 5), "env_steps_per_s": round(N * 1e3 / closed_ms, 1),
                 "lanes": env._step_lanes(),
-                "note": "BatchedPhysicsEnv.step() once per env step (HIP events on the calling stream over 20-200 "
+                "note": "BatchedPhysicsEnv.step() once per env step (HIP events on the calling stream over 200 "
                         "steps; one walker range, step()'s default): each step returns obs / reward / done / info "
                         "— what a PhysicsEnv.step caller gets; `value` is the open-loop rate (K steps issued back "
                         "to back on the ranges of run())"}

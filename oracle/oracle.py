@@ -205,3 +205,28 @@ def spec_from_npz(z) -> tuple[dict, dict]:
     params = {k[6:]: z[k].item() for k in z.files if k.startswith("param_")}
     params["action_mode"] = int(z["action_mode"])
     return spec, params
+
+
+def momentum(vel, m, mass_off) -> np.ndarray:
+    """Point.momentum of every walker (gym/engine.py:160-166): m_sum = zeros(3, float32), then m_sum += p.v * p.m
+    point by point in point order — numpy's float32 product and float32 add, restated with float32 arrays (one
+    sequential step per point index, vectorised across walkers)."""
+    vel = np.asarray(vel, np.float32).reshape(-1, 3)
+    m = np.asarray(m, np.float32)
+    mass_off = np.asarray(mass_off, np.int64)
+    N = len(mass_off) - 1
+    Ms = np.diff(mass_off)
+    out = np.zeros((N, 3), np.float32)
+    for q in range(int(Ms.max()) if N else 0):
+        sel = Ms > q
+        idx = mass_off[:-1][sel] + q
+        out[sel] = out[sel] + vel[idx] * m[idx][:, None]
+    return out
+
+
+def nonfinite(pos, vel, acc, mass_off) -> np.ndarray:
+    """1 for a walker any of whose pos / vel / acc components is inf or NaN (SURVEY §5 failure detection)."""
+    bad = ~(np.isfinite(np.asarray(pos).reshape(-1, 3)).all(1) & np.isfinite(np.asarray(vel).reshape(-1, 3)).all(1)
+            & np.isfinite(np.asarray(acc).reshape(-1, 3)).all(1))
+    mass_off = np.asarray(mass_off, np.int64)
+    return np.array([bad[a:b].any() for a, b in zip(mass_off[:-1], mass_off[1:])], np.uint8)

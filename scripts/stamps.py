@@ -3,7 +3,7 @@
 (profiling aid, not product).
 
     python scripts/variant_ab.py build stamps=-DWG_STAMPS     # here
-    python scripts/stamps.py [build_ab/lib_stamps.so]         # GPU box: one full-batch canonical launch
+    python scripts/stamps.py [ab_session/lib_stamps.so]         # GPU box: one full-batch canonical launch
 
 Stamps (s_memtime, shader clock) per wave: 0 entry, 1 loads issued, 2 loads landed + act done, 3 springs done,
 4 masses + integrator done, 5 reductions + state stores issued, 6 obs streamed.  Prints the mean phase durations,
@@ -17,7 +17,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-os.environ["WALKER_HIP_LIB"] = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "build_ab", "lib_stamps.so")
+os.environ["WALKER_HIP_LIB"] = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "ab_session", "lib_stamps.so")
 import torch  # noqa: E402
 
 from bench import make_spec  # noqa: E402

@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
 """Compile-time A/B of the step kernel (profiling aid, not product).
 
-    python scripts/variant_ab.py build NAME=FLAGS ...     # here (CPU): build_ab/lib_NAME.so, e.g.
+    python scripts/variant_ab.py build NAME=FLAGS ...     # here (CPU): ab_session/lib_NAME.so, e.g.
                                                           #   base= slow=-DWG_FAST_SPRING=0 abl1=-DWG_ABLATE=1
     python scripts/variant_ab.py run [rounds] [workload] [NAME:ENV=V,ENV=V ...]
-                                                          # GPU box: every .so in build_ab/ plus env variants of the
+                                                          # GPU box: every .so in ab_session/ plus env variants of the
                                                           # in-tree library, interleaved rounds
 
 Each (variant, round) runs in its own process (WALKER_HIP_LIB picks the library) on the bench workload and
@@ -20,7 +20,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-OUT = os.path.join(ROOT, "build_ab")
+OUT = os.path.join(ROOT, "ab_session")   # git-ignored; emptied after each A/B session
 
 
 def build(specs):

@@ -310,10 +310,13 @@ class RefRun:
             s.steps += 1
 
 
-def record(run: RefRun, spec_fn, T, actions, noise=None):
-    """Run T steps; returns dict of stacked per-step outputs (plus reset observation)."""
+def record(run: RefRun, spec_fn, T, actions, noise=None, momentum=False):
+    """Run T steps; returns dict of stacked per-step outputs (plus reset observation).  momentum: also record each
+    walker's Point.momentum() (gym/engine.py:160-166) over its own points after every step (out_momentum)."""
     rec = {k: [] for k in ("pos", "vel", "acc", "mx", "contact", "obs", "reward", "done", "centroid",
                            "energy", "steps")}
+    if momentum:
+        rec["momentum"] = []
     if noise is not None:
         run.noise(noise)
     obs0 = run.observe()
@@ -333,6 +336,15 @@ def record(run: RefRun, spec_fn, T, actions, noise=None):
         rec["contact"].append(np.array(con, np.uint8))
         rec["obs"].append(pad_obs(obs)); rec["reward"].append(r); rec["done"].append(d)
         rec["centroid"].append(cen); rec["energy"].append(en); rec["steps"].append(st)
+        if momentum:
+            E, mom = run.E, []
+            saved = E.Point.points
+            for cr in run.cr:
+                E.Point.points = list(cr.phys)
+                with np.errstate(all="ignore"):   # a diverged walker's momentum is inf / NaN, as the reference's
+                    mom.append(np.asarray(E.Point.momentum(), f32))
+            E.Point.points = saved
+            rec["momentum"].append(np.array(mom, f32))
     out = {"out_" + k: np.stack(v) for k, v in rec.items()}
     out["out_obs0"] = pad_obs(obs0)
     out["out_obs_len"] = np.array([len(o) for o in obs0], np.int32)
@@ -434,8 +446,8 @@ class Ctx:
         self.E.Point.points = []
         self.E.Point.r_points = {}
 
-    def save(self, name, run, spec, T, actions, noise=None, extra=None, action_mode="cont"):
-        outs = record(run, None, T, actions, noise)
+    def save(self, name, run, spec, T, actions, noise=None, extra=None, action_mode="cont", momentum=False):
+        outs = record(run, None, T, actions, noise, momentum)
         blob = {}
         blob.update(spec.arrays())
         blob.update(params_array(run.p))
@@ -493,6 +505,21 @@ def sc_box(c):
     spec = spec_from_creatures(crs, None)
     acts = scenario_rng("box_3d").uniform(-20, 20, (100, 2, 4)).astype(f32)
     c.save("box_3d", RefRun(c.E, c.OW, c.OE, crs, dict(in3d=1)), spec, 100, acts)
+
+
+@scenario("info_extras")
+def sc_info_extras(c):
+    """Opt-in info (ABI 10): a mixed batch — two Box-v0 walkers whose state goes non-finite at step 37 (as in box_3d)
+    beside two Balance-v0 walkers — 60 steps, with every walker's Point.momentum() (gym/engine.py:160-166) over its
+    own points after each step (out_momentum); the non-finite flag is read off out_pos / out_vel / out_acc."""
+    c.fresh()
+    crs = reference_builders(c.E, c.OW, "box", 2) + reference_builders(c.E, c.OW, "balance", 2)
+    spec = spec_from_creatures(crs, None)
+    rng = scenario_rng("info_extras")
+    acts = np.zeros((60, 4, 4), f32)
+    acts[:, :2] = rng.uniform(-20, 20, (60, 2, 4))
+    acts[:, 2:, :2] = rng.uniform(-1, 1, (60, 2, 2))
+    c.save("info_extras", RefRun(c.E, c.OW, c.OE, crs, dict(in3d=1)), spec, 60, acts, momentum=True)
 
 
 @scenario("canonical")

@@ -34,9 +34,11 @@ def _worker(rank, world, port, n_total, T, out_q, by_size, pipelined=False):
     acts = np.random.default_rng(4).uniform(-1, 1, (T, n_total, 8)).astype(np.float32)
     a, b = shard_bounds(n_total, world, rank)
     orc = Oracle(shard_spec(spec, a, b), dict(in3d=1))
-    obs = None
+    obs, rew, done = None, [], []
     for t in range(T):
-        obs = orc.step(acts[t, a:b])["obs"]
+        o = orc.step(acts[t, a:b])
+        obs = o["obs"]
+        rew.append(o["reward"]); done.append(o["done"])
     if pipelined:
         # bench.py's pipelined gather: issue the gather of this rollout's final observations, keep stepping (the next
         # rollout; the oracle writes fresh arrays, so the gathered buffer is not touched), then wait
@@ -46,8 +48,11 @@ def _worker(rank, world, port, n_total, T, out_q, by_size, pipelined=False):
         full = h.wait()
     else:
         full = gather_rollout(torch.from_numpy(obs), n_total=None if by_size else n_total)
+    # the per-step records of SURVEY §8(e) ([T, n_r] -> [T, N], dim 1), as bench.py's rollout gather sends them
+    rew_full = gather_rollout(torch.from_numpy(np.stack(rew)), n_total=None if by_size else n_total, dim=1)
+    done_full = gather_rollout(torch.from_numpy(np.stack(done)), n_total=None if by_size else n_total, dim=1)
     if rank == 0:
-        out_q.put(full.numpy())
+        out_q.put((full.numpy(), rew_full.numpy(), done_full.numpy()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -62,10 +67,12 @@ def test_shard_bounds_cover():
 
 
 @pytest.mark.parametrize("world,n_total,by_size,pipelined", [(2, 64, False, False), (2, 65, False, False),
-                                                             (3, 65, True, False), (2, 65, False, True)])
+                                                             (3, 65, True, False), (2, 65, False, True),
+                                                             (8, 1003, False, False), (8, 1003, True, False)])
 def test_gloo_matches_single_process(world, n_total, by_size, pipelined):
-    """Even and uneven shards (65 walkers: ranks of 33/32 or 22/22/21), lengths from shard_bounds or gathered; the
-    pipelined form (gather issued, more steps, then waited) gathers the same rows."""
+    """Even and uneven shards (65 walkers: ranks of 33/32 or 22/22/21; config 4's world of 8 with 1,003 walkers:
+    ranks of 126 / 125), lengths from shard_bounds or gathered; the pipelined form (gather issued, more steps, then
+    waited) gathers the same rows; the per-step rewards and done flags gather along their walker axis."""
     from oracle.oracle import Oracle
     from walker_gym_amd.synthetic import canonical_walkers
     T = 5
@@ -76,14 +83,19 @@ def test_gloo_matches_single_process(world, n_total, by_size, pipelined):
              for r in range(world)]
     for p in procs:
         p.start()
-    got = q.get(timeout=180)
+    got, got_rew, got_done = q.get(timeout=180)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     spec = canonical_walkers(n_total, seed=4)
     acts = np.random.default_rng(4).uniform(-1, 1, (T, n_total, 8)).astype(np.float32)
     orc = Oracle(spec, dict(in3d=1))
+    rew, done = [], []
     for t in range(T):
-        ref = orc.step(acts[t])["obs"]
+        o = orc.step(acts[t])
+        ref = o["obs"]
+        rew.append(o["reward"]); done.append(o["done"])
     assert got.shape == ref.shape
     assert np.array_equal(got, ref)
+    assert np.array_equal(got_rew.view(np.uint32), np.stack(rew).view(np.uint32))
+    assert np.array_equal(got_done, np.stack(done))

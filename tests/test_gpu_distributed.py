@@ -55,12 +55,14 @@ def test_two_ranks_bitwise_equal_one_rank_and_oracle(tmp_path, n_total):
         assert g[k].shape == v.shape, k
         assert np.array_equal(np.ascontiguousarray(g[k]).view(np.uint8), np.ascontiguousarray(v).view(np.uint8)), k
     orc = Oracle(spec, dict(in3d=1))
+    bits = lambda a: np.ascontiguousarray(a).view(np.uint8)
     for t in range(T):
         ref = orc.step(acts[t])
-        np.testing.assert_allclose(one["obs"][t], ref["obs"], atol=1e-4, rtol=1e-5)
-        np.testing.assert_allclose(one["reward"][t], ref["reward"], atol=1e-4, rtol=1e-5)
+        np.testing.assert_allclose(one["obs"][t], ref["obs"], atol=1e-4, rtol=1e-5)   # the stated contract, then bits
+        assert np.array_equal(bits(one["obs"][t]), bits(ref["obs"])), t
+        assert np.array_equal(bits(one["reward"][t]), bits(ref["reward"])), t
         assert np.array_equal(one["done"][t], ref["done"])
-    np.testing.assert_allclose(one["pos"].reshape(-1, 3), orc.pos, atol=1e-4, rtol=1e-5)
+    assert np.array_equal(bits(one["pos"].reshape(-1, 3)), bits(orc.pos))
 
 
 def test_rccl_one_rank_gather_rollout_on_device(tmp_path):

@@ -13,7 +13,7 @@ import threading
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libwalker_hip.so"
 LIB_PATH = os.path.join(HERE, LIB_NAME)
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 WG_EINVAL, WG_ERANGE, WG_EHIP = -1, -2, -3
 
@@ -46,7 +46,7 @@ class WgBatch(C.Structure):
 class WgOutputs(C.Structure):
     _fields_ = [("obs", _vp), ("obs_stride", C.c_int32), ("reward", _vp), ("done", _vp),
                 ("centroid", _vp), ("energy", _vp), ("obs_step", C.c_int64), ("out_step", C.c_int64),
-                ("obs_pad_clean", C.c_int32), ("steps", _vp)]
+                ("obs_pad_clean", C.c_int32), ("steps", _vp), ("nonfinite", _vp), ("momentum", _vp)]
 
 
 class WgRange(C.Structure):

@@ -98,20 +98,26 @@ class WalkerGraph:
     radii bump the env's generation, and replay() of a graph captured before that raises instead of writing
     into freed memory or silently stepping with stale parameters."""
 
-    def __init__(self, env: "BatchedPhysicsEnv", graph, actions):
+    def __init__(self, env: "BatchedPhysicsEnv", graph, actions, info: bool = True):
         self._env, self._graph, self._gen = env, graph, env._generation
         self.actions = actions            # kept alive: the graph reads it on every replay
+        # the replayed steps write info['steps'] in caller order (env.steps_out) only when captured with info
+        self._writes_steps = bool(info) and env.steps_out is not None
 
     def replay(self) -> None:
-        if self._env._generation != self._gen:
+        env = self._env
+        if env._generation != self._gen:
             raise RuntimeError("stale WalkerGraph: the env's parameters or buffers changed after capture; "
                                "capture a new graph")
         self._graph.replay()
+        # the batch's step counters moved: steps_out is current only if the graph wrote it (ADVICE r3: a graph
+        # captured with info=False left a step()'s steps_out looking valid)
+        env._steps_at = env.batch.version if self._writes_steps else -1
 
 
 class BatchedPhysicsEnv:
     def __init__(self, spec_or_layout, device=None, rand_sigma: float = 0.0, seed: Optional[int] = None,
-                 contact: bool = True, **params):
+                 contact: bool = True, info_extras: bool = False, **params):
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else None
         if device is None:
@@ -135,6 +141,9 @@ class BatchedPhysicsEnv:
         if seed is not None:
             self._gen.manual_seed(int(seed))
         self._generation = 0
+        # opt-in info (ABI 10): info['momentum'] (Point.momentum per walker, gym/engine.py:160-166) and
+        # info['nonfinite'] (a walker whose state holds an inf / NaN; done is left as the reference computes it)
+        self._extras = bool(info_extras)
         self._alloc_outputs()
         # the side streams of the default walker ranges, created now: a stream's hardware queue is bound when it is
         # created, and a process has few of them (GPU_MAX_HW_QUEUES = 4).  Created after an RCCL communicator
@@ -184,13 +193,30 @@ class BatchedPhysicsEnv:
         # (wg_outputs.steps) so that step() needs no gather; valid while _steps_at == the batch's state version
         self.steps_out = torch.zeros(N, dtype=torch.int32, device=dv) if self.batch._perm else None
         self._steps_at = -1
+        self.momentum = torch.zeros((N, 3), dtype=torch.float32, device=dv) if self._extras else None
+        self.nonfinite = torch.zeros(N, dtype=torch.bool, device=dv) if self._extras else None
+
+    def enable_info_extras(self) -> None:
+        """Start producing info['momentum'] and info['nonfinite'] every step (one small per-walker pass after the
+        step kernel).  Graphs captured before this raise on replay (the outputs were reallocated)."""
+        if not self._extras:
+            self._extras = True
+            self._alloc_outputs()
 
     def _outputs(self, obs=None, reward=None, done=None, centroid=None, energy=None, obs_step=0, out_step=0,
-                 pad_clean=False, steps=None):
+                 pad_clean=False, steps=None, nonfinite=None, momentum=None):
         p = lambda t: None if t is None else C.c_void_p(t.data_ptr())
         return _lib.WgOutputs(obs=p(obs), obs_stride=self.obs_dim, reward=p(reward), done=p(done),
                               centroid=p(centroid), energy=p(energy), obs_step=obs_step, out_step=out_step,
-                              obs_pad_clean=int(pad_clean), steps=p(steps))
+                              obs_pad_clean=int(pad_clean), steps=p(steps), nonfinite=p(nonfinite),
+                              momentum=p(momentum))
+
+    def _extra_out(self, w0: int = 0, w1: Optional[int] = None) -> dict:
+        """The opt-in info outputs of walkers [w0, w1) (or none)."""
+        if not self._extras:
+            return {}
+        w1 = self.N if w1 is None else w1
+        return {"nonfinite": self.nonfinite[w0:w1], "momentum": self.momentum[w0:w1]}
 
     def _stream(self):
         return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
@@ -259,7 +285,7 @@ class BatchedPhysicsEnv:
         if rc:
             _lib.check(rc, "wg_step_ranges")
         self._steps_at = self.batch.version
-        if act is not None and plan["n"] > 1:
+        if act is not None and plan["n"] > 1 and not torch.cuda.is_current_stream_capturing():
             for st in plan["side"]:
                 act.record_stream(st)   # the allocator must not recycle the actions before the side streams read them
         return self.obs, self.reward, self.done, self.info()
@@ -281,7 +307,8 @@ class BatchedPhysicsEnv:
         def out(w0, w1):
             o = self._outputs(self.obs[w0:w1], self.reward[w0:w1], self.done[w0:w1], self.centroid[w0:w1],
                               self.energy[w0:w1], pad_clean=True,
-                              steps=None if self.steps_out is None else self.steps_out[w0:w1])
+                              steps=None if self.steps_out is None else self.steps_out[w0:w1],
+                              **self._extra_out(w0, w1))
             keep.append(o)
             return C.pointer(o)
         if lanes == 1 or b.ragged:
@@ -352,10 +379,16 @@ class BatchedPhysicsEnv:
             self.batch.plan_blocks, self._stream()), entry)
         return obs_out, reward_out, done_out
 
-    def run(self, actions, n_steps: int, info: bool = True, lanes: Optional[int] = None, resident: bool = False):
+    def run(self, actions, n_steps: int, info: bool = True, lanes: Optional[int] = None, resident: bool = False,
+            record: Optional[dict] = None):
         """Throughput path: n_steps env steps in one C call; step s acts with actions[s % T]
         ([T, N, A] device tensor; T == n_steps or 1) and overwrites obs/reward/done(/info) each step.  resident:
-        wg_rollout (one launch for all steps where the batch allows it) instead of one launch per step."""
+        wg_rollout (one launch for all steps where the batch allows it) instead of one launch per step.
+
+        record: every step's reward / done (and with info, energy / centroid) into caller buffers instead of the
+        env's one-step outputs — {'reward': [n_steps, N] f32, 'done': [n_steps, N] bool or u8, optionally 'energy'
+        [n_steps, N] f32 and 'centroid' [n_steps, N, 3] f32} — while obs keeps the last step's rows (env.obs): the
+        rollout SURVEY §8(e) gathers at its end.  The same bytes as a plain run, written at per-step offsets."""
         require_tensor(actions, "actions", self.device, torch.float32)
         if actions.dim() != 3:
             raise ValueError("actions must be a contiguous [n_steps or 1, N, A] device tensor")
@@ -365,15 +398,35 @@ class BatchedPhysicsEnv:
         lanes = self._lanes(1 if (resident and lanes is None and self.resident_ok()) else lanes)
         entry = "wg_rollout" if resident else "wg_step"
         so = self.steps_out if info else None
+        rew, done, cen, en, out_step = self.reward, self.done, self.centroid, self.energy, 0
+        if record is not None:
+            S = int(n_steps)
+            rew, done = record["reward"], record["done"]
+            require_tensor(rew, "record['reward']", self.device, torch.float32, (S, self.N))
+            if not isinstance(done, torch.Tensor) or done.dtype not in (torch.bool, torch.uint8):
+                raise ValueError("record['done'] must be a bool or uint8 tensor")
+            require_tensor(done, "record['done']", self.device, done.dtype, (S, self.N))
+            cen, en = record.get("centroid"), record.get("energy")
+            if cen is not None:
+                require_tensor(cen, "record['centroid']", self.device, torch.float32, (S, self.N, 3))
+            if en is not None:
+                require_tensor(en, "record['energy']", self.device, torch.float32, (S, self.N))
+            rew, done = rew[0], done[0]
+            cen, en = (None if cen is None else cen[0]), (None if en is None else en[0])
+            so, out_step = None, self.N   # (the steps output would need [n_steps, N] too: info() gathers them)
+        if not info:
+            cen = en = None
+        # the opt-in info extras follow the last step only when the outputs are overwritten each step (no record)
+        ex = (lambda w0, w1: self._extra_out(w0, w1)) if (info and record is None) else (lambda w0, w1: {})
         if lanes > 1:
             self._run_lanes(actions, int(n_steps), lambda w0, w1: self._outputs(
-                self.obs[w0:w1], self.reward[w0:w1], self.done[w0:w1], self.centroid[w0:w1] if info else None,
-                self.energy[w0:w1] if info else None, pad_clean=True, steps=None if so is None else so[w0:w1]),
-                lanes, entry=entry)
+                self.obs[w0:w1], rew[w0:w1], done[w0:w1], None if cen is None else cen[w0:w1],
+                None if en is None else en[w0:w1], pad_clean=True, steps=None if so is None else so[w0:w1],
+                out_step=out_step, **ex(w0, w1)), lanes, entry=entry)
             self._steps_at = self.batch.version if so is not None else -1
             return
-        o = self._outputs(self.obs, self.reward, self.done, self.centroid if info else None,
-                          self.energy if info else None, pad_clean=True, steps=so)
+        o = self._outputs(self.obs, rew, done, cen, en, pad_clean=True, steps=so, out_step=out_step,
+                          **ex(0, self.N))
         _lib.check(getattr(_lib.load(), entry)(
             C.byref(self.batch.struct), C.byref(self._pstruct), C.c_void_p(actions.data_ptr()), cols, cols,
             0 if T == 1 else self.N * cols, C.byref(o), int(n_steps),
@@ -468,14 +521,17 @@ class BatchedPhysicsEnv:
         g = torch.cuda.CUDAGraph()
         side = torch.cuda.Stream(device=self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
+        steps_at = self._steps_at               # capture runs nothing: the outputs' validity is unchanged by it
         with torch.cuda.stream(side):           # capture off the default stream, as torch requires
             with torch.cuda.graph(g, stream=side):
                 self.run(actions, n_steps, info=info, lanes=lanes)
         torch.cuda.current_stream(self.device).wait_stream(side)
-        return WalkerGraph(self, g, actions)
+        self._steps_at = steps_at
+        return WalkerGraph(self, g, actions, info=info)
 
     def observe(self):
-        o = self._outputs(self.obs, self.reward, self.done, self.centroid, self.energy, steps=self.steps_out)
+        o = self._outputs(self.obs, self.reward, self.done, self.centroid, self.energy, steps=self.steps_out,
+                          **self._extra_out())
         _lib.check(_lib.load().wg_observe(
             C.byref(self.batch.struct), C.byref(self._pstruct), C.byref(o),
             None if self.batch.plan is None else C.c_void_p(self.batch.plan.data_ptr()),
@@ -509,7 +565,11 @@ class BatchedPhysicsEnv:
             steps = self.steps_out                 # written by the last step / observe in caller order
         else:
             steps = self.batch.caller("steps")     # a gather (after a rollout, a reset mask, or loaded state)
-        return {"steps": steps, "centroid_position": self.centroid, "total_energy": self.energy}
+        info = {"steps": steps, "centroid_position": self.centroid, "total_energy": self.energy}
+        if self._extras:
+            info["momentum"] = self.momentum      # Point.momentum (gym/engine.py:160-166) of each walker
+            info["nonfinite"] = self.nonfinite    # True: the walker's pos / vel / acc hold an inf or NaN
+        return info
 
     # state accessors in the caller's order.  An unpermuted batch returns live views into its tensors; a ragged batch
     # (stored in wave-tile / size order) returns gathered COPIES, so in-place writes into them do not reach the batch:

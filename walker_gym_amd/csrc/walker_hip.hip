@@ -2677,6 +2677,35 @@ __global__ void walker_reset_kernel(wg_batch b, const float *__restrict__ noise,
         if (!mask || mask[w]) b.steps[w] = 0;
 }
 
+// Opt-in per-walker info of the state after a step or observe (wg_outputs.nonfinite / momentum, ABI 10): one lane
+// per walker walks its masses in point order.  nonfinite: any pos / vel / acc component inf or NaN (SURVEY §5 failure
+// detection; done is untouched).  momentum: Point.momentum (gym/engine.py:160-166), m_sum = float32 zeros, then
+// m_sum += v * m point by point (v float32, m the point's mass: numpy's float32 product, then a float32 add).
+// Outputs at the caller's row (wg_batch.row).  Not on the headline path: a caller that asks for neither pays nothing.
+// A ragged batch's walker range is its plan slice [plan[0], plan[plan_blocks]) (the other ranges of a wg_step_ranges
+// call may still be stepping theirs).
+__global__ __launch_bounds__(256) void walker_info_kernel(wg_batch b, uint8_t *__restrict__ nonfinite,
+                                                          float *__restrict__ momentum, const int32_t *__restrict__ plan,
+                                                          int plan_blocks) {
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= b.N) return;
+    if (plan && (w < plan[0] || w >= plan[plan_blocks])) return;
+    const int p0 = b.ragged ? b.mass_off[w] : w * b.M, p1 = b.ragged ? b.mass_off[w + 1] : p0 + b.M;
+    float mx = 0.f, my = 0.f, mz = 0.f;
+    bool bad = false;
+    for (int q = p0; q < p1; q++) {
+        const float *pv = b.pos + 3 * (size_t)q, *vv = b.vel + 3 * (size_t)q, *av = b.acc + 3 * (size_t)q;
+        const float vx = vv[0], vy = vv[1], vz = vv[2], m = b.mass[q];
+        bad = bad || !(__builtin_isfinite(pv[0]) && __builtin_isfinite(pv[1]) && __builtin_isfinite(pv[2]) &&
+                       __builtin_isfinite(vx) && __builtin_isfinite(vy) && __builtin_isfinite(vz) &&
+                       __builtin_isfinite(av[0]) && __builtin_isfinite(av[1]) && __builtin_isfinite(av[2]));
+        mx = mx + vx * m; my = my + vy * m; mz = mz + vz * m;
+    }
+    const int r = caller_row(b, w);
+    if (nonfinite) nonfinite[r] = (uint8_t)bad;
+    if (momentum) { momentum[3 * r] = mx; momentum[3 * r + 1] = my; momentum[3 * r + 2] = mz; }
+}
+
 // ------------------------------------------------------------------ host side
 int env_int(const char *name, int dflt);
 int wave_passes(int M, int K);
@@ -2996,7 +3025,7 @@ int dispatch(const wg_batch *b, const KParams &kp, bool in3d, const float *a, in
 
 int run(const wg_batch *b, const wg_params *p, const float *action, int32_t cols, int32_t astride,
         int64_t astep, const wg_outputs *o, int32_t n_steps, const int32_t *plan, int32_t plan_blocks,
-        hipStream_t stream, bool step, bool resident = false) {
+        hipStream_t stream, bool step, bool resident = false, bool check_only = false) {
     int rc = validate(b);
     if (rc) return rc;
     if (!p) return fail(WG_EINVAL, "null params");
@@ -3027,7 +3056,18 @@ int run(const wg_batch *b, const wg_params *p, const float *action, int32_t cols
         return fail(WG_EINVAL, "pair_mode %d needs spring_mode 0", p->pair_mode);
     if (step && (p->pair_mode & 4) && !b->radius)
         return fail(WG_EINVAL, "pair_mode 4 (bounce) needs the radius array");
-    if (resident && use_lean && p->pair_mode == 0)   // one launch for every step, state in registers throughout
+    if (check_only) return 0;   // wg_step_ranges: every range's arguments checked before any range launches
+    const bool extras = out.nonfinite || out.momentum;   // opt-in per-walker info after each step (ABI 10)
+    auto info_pass = [&](const wg_outputs &os) -> int {
+        if (!(os.nonfinite || os.momentum)) return 0;
+        hipLaunchKernelGGL(walker_info_kernel, dim3((b->N + 255) / 256), dim3(256), 0, stream, *b, os.nonfinite,
+                           os.momentum, b->ragged ? plan : nullptr, plan_blocks);
+        const hipError_t e = hipGetLastError();
+        return e == hipSuccess ? 0 : fail(WG_EHIP, "info launch failed: %s", hipGetErrorString(e));
+    };
+    // (the resident rollout keeps the state in registers between steps: with the per-step info extras requested the
+    // steps run as per-step launches instead, bit-identical)
+    if (resident && use_lean && p->pair_mode == 0 && !extras)   // one launch for every step, state in registers
         return launch_lean_rollout(b, kp, p->in3d != 0, action, cols, astride, action ? astep : 0, out, n_steps, lg,
                                    stream);
     for (int s = 0; s < n_steps; s++) {
@@ -3038,20 +3078,15 @@ int run(const wg_batch *b, const wg_params *p, const float *action, int32_t cols
         if (os.energy) os.energy += s * os.out_step;
         if (os.centroid) os.centroid += 3 * s * os.out_step;
         if (os.steps) os.steps += s * os.out_step;
+        if (os.nonfinite) os.nonfinite += s * os.out_step;
+        if (os.momentum) os.momentum += 3 * s * os.out_step;
         const float *a = action ? action + s * astep : nullptr;
-        if (step && use_lean) {
-            rc = launch_lean(b, kp, p->in3d != 0, a, cols, astride, os, lg, stream);
-            if (rc) return rc;
-            continue;
-        }
-        if (use_waves) {
-            rc = launch_waves(b, kp, p->in3d != 0, a, cols, astride, os, plan, plan_blocks, rgeo, stream);
-            if (rc) return rc;
-            continue;
-        }
-        rc = step ? dispatch<true>(b, kp, p->in3d != 0, a, cols, astride, os, plan, blocks, g, stream)
-                  : dispatch<false>(b, kp, p->in3d != 0, nullptr, 0, 0, os, plan, blocks, g, stream);
+        if (step && use_lean) rc = launch_lean(b, kp, p->in3d != 0, a, cols, astride, os, lg, stream);
+        else if (use_waves) rc = launch_waves(b, kp, p->in3d != 0, a, cols, astride, os, plan, plan_blocks, rgeo, stream);
+        else rc = step ? dispatch<true>(b, kp, p->in3d != 0, a, cols, astride, os, plan, blocks, g, stream)
+                       : dispatch<false>(b, kp, p->in3d != 0, nullptr, 0, 0, os, plan, blocks, g, stream);
         if (rc) return rc;
+        if (extras && (rc = info_pass(os))) return rc;
     }
     return 0;
 }
@@ -3086,6 +3121,13 @@ int wg_rollout(const wg_batch *b, const wg_params *p, const float *action, int32
 int wg_step_ranges(const wg_range *ranges, int32_t n, const wg_params *p, const float *action, int32_t action_cols,
                    int32_t action_stride, hipEvent_t *events) {
     if (!ranges || n < 1 || (n > 1 && !events)) return fail(WG_EINVAL, "wg_step_ranges: bad ranges / events");
+    // every range checked before the first launch: a bad range fails the call with no walker stepped
+    for (int i = 0; i < n; i++) {
+        const wg_range &r = ranges[i];
+        const int rc = run(r.batch, p, action ? action + r.action_offset : nullptr, action_cols, action_stride, 0,
+                           r.outputs, 1, r.plan, r.plan_blocks, r.stream, true, false, true);
+        if (rc) return rc;
+    }
     hipStream_t s0 = ranges[0].stream;
     if (n > 1 && hipEventRecord(events[0], s0) != hipSuccess) return fail(WG_EHIP, "fork event record failed");
     for (int i = 0; i < n; i++) {

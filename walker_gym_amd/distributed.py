@@ -4,8 +4,11 @@ Walkers are independent (no inter-walker force on the env path), so a node-wide 
 contiguous walker blocks, one per rank (one process per GPU, torch.distributed over RCCL/xGMI).
 Stepping needs no communication at all; the only collective is the observation gather at the end
 of a rollout (``gather_rollout``: one all_gather_into_tensor on RCCL, all_gather on gloo; uneven
-shards are padded to the longest and trimmed).  ``gather_rollout_async`` issues it without waiting, so
-an actor loop overlaps the gather of rollout i with the steps of rollout i + 1 (bench.py's default).
+shards are padded to the longest and trimmed).  The gathered rollout is SURVEY §8(e)'s tuple: the final
+observations [N, D] and every step's reward and done flags [T, N] (``dim=1``: walkers on the second axis).
+``gather_rollout_async`` issues a gather without waiting, so an actor loop can overlap the gather of rollout i with
+the steps of rollout i + 1 (bench.py ``--gather pipelined``, opt-in: on one MI355X the concurrent RCCL kernel
+stalled the steps, DESIGN §8, so bench.py's default is ``--gather serial``).
 Results of shard g are bit-identical to the same walkers stepped on one GPU (tested).
 """
 from __future__ import annotations
@@ -51,21 +54,28 @@ class GatherHandle:
     """An issued rollout-end gather (gather_rollout_async): wait() makes the calling stream wait for the collective
     and returns the gathered [n_total, ...] tensor.  The buffers stay referenced until then."""
 
-    def __init__(self, work, out, sizes, nmax, world):
+    def __init__(self, work, out, sizes, nmax, world, dim=0):
         self._work, self._out, self._sizes, self._nmax, self._world = work, out, sizes, nmax, world
+        self._dim = dim
 
     def wait(self) -> torch.Tensor:
         if self._work is not None:
             self._work.wait()
             self._work = None
-        out, sizes, nmax = self._out, self._sizes, self._nmax
+        out, sizes, nmax, world = self._out, self._sizes, self._nmax, self._world
+        if self._dim == 1:   # [world * T, nmax, ...] rank blocks -> [T, sum(sizes), ...] (one device copy)
+            T = out.shape[0] // world
+            blk = out.view((world, T) + tuple(out.shape[1:]))
+            if all(sz == nmax for sz in sizes):
+                return blk.transpose(0, 1).reshape((T, world * nmax) + tuple(out.shape[2:]))
+            return torch.cat([blk[r, :, :sizes[r]] for r in range(world)], 1)
         if all(sz == nmax for sz in sizes):
             return out
-        return torch.cat([out[r * nmax:r * nmax + sizes[r]] for r in range(self._world)], 0)
+        return torch.cat([out[r * nmax:r * nmax + sizes[r]] for r in range(world)], 0)
 
 
 def gather_rollout_async(local: torch.Tensor, group: Optional[dist.ProcessGroup] = None,
-                         n_total: Optional[int] = None) -> GatherHandle:
+                         n_total: Optional[int] = None, dim: int = 0) -> GatherHandle:
     """Issue the rollout-end gather (every rank's [n_r, ...] block concatenated along dim 0 in rank order) without
     waiting for it: on RCCL the collective runs on the process group's own stream, ordered after the work already
     queued on the calling stream, so steps issued afterwards overlap it (an actor loop gathers rollout i while
@@ -74,10 +84,15 @@ def gather_rollout_async(local: torch.Tensor, group: Optional[dist.ProcessGroup]
     Blocks may differ in length (shard_bounds gives the first n_total % world ranks one walker more): each block is
     padded to the longest, gathered with one collective (all_gather_into_tensor on RCCL, all_gather on gloo) and
     trimmed.  The lengths come from shard_bounds when ``n_total`` is given, otherwise from a small (synchronous)
-    all_gather of every rank's length."""
+    all_gather of every rank's length.
+
+    dim = 1: `local` is a per-step record [T, n_r, ...] (rewards, done flags); the rank blocks are gathered whole
+    (each rank's [T, nmax, ...] is one contiguous send buffer, no transpose copy) and returned as [T, N, ...]."""
+    if dim not in (0, 1):
+        raise ValueError("dim must be 0 (walker rows) or 1 ([T, walkers, ...] records)")
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    n = int(local.shape[0])
+    n = int(local.shape[dim])
     if n_total is not None:
         sizes = [b - a for a, b in (shard_bounds(n_total, world, r) for r in range(world))]
         if sizes[rank] != n:
@@ -90,19 +105,22 @@ def gather_rollout_async(local: torch.Tensor, group: Optional[dist.ProcessGroup]
     nmax = max(sizes)
     block = local.contiguous()
     if n < nmax:
-        block = torch.cat([block, block.new_zeros((nmax - n,) + tuple(local.shape[1:]))], 0)
-    out = torch.empty((world * nmax,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+        pad = list(local.shape)
+        pad[dim] = nmax - n
+        block = torch.cat([block, block.new_zeros(pad)], dim)
+    lead = block.shape[0]
+    out = torch.empty((world * lead,) + tuple(block.shape[1:]), dtype=local.dtype, device=local.device)
     if dist.get_backend(group) == "nccl":
         work = dist.all_gather_into_tensor(out, block, group=group, async_op=True)
     else:
         work = dist.all_gather(list(out.chunk(world, 0)), block, group=group, async_op=True)
-    h = GatherHandle(work, out, sizes, nmax, world)
+    h = GatherHandle(work, out, sizes, nmax, world, dim)
     h._block = block   # (the padded copy, if any, lives until wait)
     return h
 
 
 def gather_rollout(local: torch.Tensor, group: Optional[dist.ProcessGroup] = None,
-                   n_total: Optional[int] = None) -> torch.Tensor:
-    """Concatenate every rank's [n_r, ...] block along dim 0, in rank order — the rollout-end gather
+                   n_total: Optional[int] = None, dim: int = 0) -> torch.Tensor:
+    """Concatenate every rank's block along the walker axis `dim`, in rank order — the rollout-end gather
     (gather_rollout_async, waited for at once)."""
-    return gather_rollout_async(local, group, n_total).wait()
+    return gather_rollout_async(local, group, n_total, dim).wait()

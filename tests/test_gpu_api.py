@@ -98,3 +98,33 @@ def test_demo_runs(args, head):
     line = r.stdout.strip().splitlines()[-1]
     assert line.startswith(head), line
     assert "nan" not in line.lower(), line
+
+
+def test_step_ranges_validates_every_range_before_launching():
+    """wg_step_ranges checks every range's arguments before the first launch: a bad second range fails
+    the call with no walker of the first range stepped."""
+    import ctypes as C
+    import numpy as np
+    import torch
+    from walker_gym_amd import _lib
+    from walker_gym_amd.batched_env import BatchedPhysicsEnv
+    from walker_gym_amd.synthetic import canonical_walkers
+    env = BatchedPhysicsEnv(canonical_walkers(256, seed=3), device="cuda:0", in3d=1)
+    before = env.pos.clone()
+    steps0 = env.steps.clone()
+    L = _lib.load()
+    b = env.batch
+    good, o = b.sub_struct(0, 128), env._outputs(env.obs[:128], env.reward[:128], env.done[:128])
+    bad = b.sub_struct(128, 256)
+    bad.M = 0                                   # invalid: the second range's own checks fail
+    rng = (_lib.WgRange * 2)()
+    rng[0].batch, rng[0].outputs, rng[0].stream = C.pointer(good), C.pointer(o), torch.cuda.current_stream().cuda_stream
+    rng[1].batch, rng[1].outputs, rng[1].stream = C.pointer(bad), C.pointer(o), torch.cuda.current_stream().cuda_stream
+    evs = [torch.cuda.Event() for _ in range(2)]
+    for e in evs:
+        e.record()
+    events = (C.c_void_p * 2)(*[e.cuda_event for e in evs])
+    rc = L.wg_step_ranges(rng, 2, C.byref(env._pstruct), None, 0, 0, events)
+    torch.cuda.synchronize()
+    assert rc == _lib.WG_EINVAL
+    assert torch.equal(env.pos, before) and torch.equal(env.steps, steps0)

@@ -338,6 +338,18 @@ def test_info_steps_caller_order_without_gather():
     env.step(acts[5])
     env.batch.load_state_dict(sd)
     assert torch.equal(check(False), got)
+    # graph replay: after a step() (steps_out valid), a graph captured with info=False advances the
+    # counters without writing steps_out, so info() must gather; one captured with info=True keeps steps_out current
+    env.step(acts[0])
+    check(True)
+    g0 = env.graph(acts[1:3].contiguous(), 2, info=False)
+    check(True)                          # capture runs nothing
+    g0.replay()
+    after = check(False)
+    assert torch.equal(after, got + 3)
+    g1 = env.graph(acts[1:3].contiguous(), 2, info=True)
+    g1.replay()
+    assert torch.equal(check(True), got + 5)
 
 
 @pytest.mark.gpu

@@ -416,6 +416,53 @@ def main():
             e1.record(stream)
             torch.cuda.synchronize()
             closed_ms = e0.elapsed_time(e1) / n_cl
+        # closed loop with a policy (every action a function of the current observation): a row-wise policy, tanh of
+        # each walker's observed muscle lengths, driven (a) by step() in a loop — one barrier per step — and (b) by
+        # policy_loop, the walker ranges pipelined (each range acts on its own rows and steps on its own stream);
+        # (a) and (b) give bit-identical trajectories
+        policy_cl = None
+        if not args.no_control and not env.batch.ragged and args.workload not in PAIR_FLOP:
+            Acols = env.batch.A
+            pol = lambda rows, t: torch.tanh(rows[:, rows.shape[1] - Acols:])
+            for _ in range(3):
+                env.step(pol(env.obs, 0))
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for s_ in range(n1):
+                env.step(pol(env.obs, s_))
+            e1.record(stream)
+            torch.cuda.synchronize()
+            step_pol_ms = e0.elapsed_time(e1) / n1
+            env.policy_loop(pol, 5, lanes=lanes)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            env.policy_loop(pol, n1, lanes=lanes)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            ranges_ms = e0.elapsed_time(e1) / n1
+            env.policy_loop(pol, 5, lanes=lanes, graph=True)    # warm the capture path
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            env.policy_loop(pol, n1, lanes=lanes, graph=True)   # (capture on the host, then one replay)
+            torch.cuda.synchronize()
+            g = env._policy_graph
+            e0.record(stream)
+            g.replay()
+            e1.record(stream)
+            torch.cuda.synchronize()
+            ranges_graph_ms = e0.elapsed_time(e1) / n1
+            policy_cl = {"policy": "action = tanh(the walker's own observed muscle lengths), one elementwise kernel per "
+                                   "call (row-wise)", "steps": n1,
+                         "step_loop_ms_per_step": round(step_pol_ms, 5),
+                         "policy_loop_ms_per_step": round(ranges_ms, 5),
+                         "policy_loop_graph_ms_per_step": round(ranges_graph_ms, 5),
+                         "lanes": lanes,
+                         "note": "step_loop: BatchedPhysicsEnv.step(policy(obs)) per env step (a full barrier per step: each "
+                                 "launch drains alone); policy_loop: the walker ranges pipelined, each range's policy "
+                                 "and step on its own stream (bit-identical trajectories, tests/test_gpu_policy_loop.py); "
+                                 "graph: the same loop captured as one HIP graph and replayed (HIP events around the "
+                                 "replay)"}
         resident_ms = None
         if args.resident:
             env.run(acts_c, n1, lanes=1, resident=True)
@@ -497,6 +544,9 @@ def main():
                         "steps; one walker range, step()'s default): each step returns obs / reward / done / info "
                         "— what a PhysicsEnv.step caller gets; `value` is the open-loop rate (K steps issued back "
                         "to back on the ranges of run())"}
+        if policy_cl is not None:
+            policy_cl["open_loop_ms_per_step"] = round(step_ms, 5)
+            line["closed_loop_policy"] = policy_cl
         if resident_ms is not None:
             line["resident_rollout"] = {
                 "ms_per_step": round(resident_ms, 5), "env_steps_per_s": round(N * 1e3 / resident_ms, 1),

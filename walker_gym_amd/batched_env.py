@@ -512,6 +512,70 @@ class BatchedPhysicsEnv:
         for ev in done:
             cur.wait_event(ev)
 
+    def policy_loop(self, policy, n_steps: int, lanes: Optional[int] = None, graph: bool = False) -> None:
+        """A closed loop with a per-walker policy, the walker ranges pipelined: at every step, each range computes its
+        actions from ITS OWN current observation rows, action = policy(obs[w0:w1], t), and launches its step right
+        after, on its own stream; the ranges never wait for one another.  So one range's step t + 1 fills the other's
+        launch tail, as in the open-loop run(), while every action still depends on the observation it follows.
+        step() in a loop cannot do that: it returns the whole batch's obs, so each step ends at a full barrier and
+        each launch drains on its own (the drain is what separates one launch from two overlapped ranges).
+
+        policy(obs_rows [n_r, D] view, t) -> actions [n_r, A_cols] float32, contiguous, on the current (range)
+        stream.  It must be row-wise — walker w's action a function of walker w's observation only — which is what
+        makes the ranges independent; then the results are bit-identical to `for t: env.step(policy(env.obs, t))`.
+        graph=True captures the n_steps x ranges loop (policy kernels included) as one HIP graph and replays it once
+        (no per-step host cost; the policy must be capturable).  Uniform batches (a ragged range's rows are not
+        contiguous in the caller's order).  After the call obs / reward / done / info hold the last step's outputs."""
+        if self.batch.ragged:
+            raise ValueError("policy_loop: uniform batches only (a ragged walker range is not a row slice)")
+        lanes = self._lanes(lanes)
+        bounds = [0] + [((self.N * i // lanes) + 63) // 64 * 64 for i in range(1, lanes)] + [self.N]
+        self.reserve_streams(lanes)
+        L = _lib.load()
+        ranges = []
+        for i in range(lanes):
+            w0, w1 = bounds[i], bounds[i + 1]
+            sub = self.batch.sub_struct(w0, w1)
+            o = self._outputs(self.obs[w0:w1], self.reward[w0:w1], self.done[w0:w1], self.centroid[w0:w1],
+                              self.energy[w0:w1], pad_clean=True, **self._extra_out(w0, w1))
+            ranges.append((w0, w1, sub, o))
+
+        def body(cur):
+            streams = [cur] + self._side[:lanes - 1]
+            start = torch.cuda.Event()
+            start.record(cur)
+            for st in streams[1:]:
+                st.wait_event(start)
+            for t in range(int(n_steps)):
+                for (w0, w1, sub, o), st in zip(ranges, streams):
+                    with torch.cuda.stream(st):
+                        a = policy(self.obs[w0:w1], t)
+                        require_tensor(a, "policy actions", self.device, torch.float32)
+                        if a.dim() != 2 or a.shape[0] != w1 - w0:
+                            raise ValueError(f"policy returned {tuple(a.shape)}, expected [{w1 - w0}, A]")
+                        cols = int(a.shape[1])
+                        _lib.check(L.wg_step(C.byref(sub), C.byref(self._pstruct), C.c_void_p(a.data_ptr()), cols,
+                                             cols, 0, C.byref(o), 1, None, 0, C.c_void_p(st.cuda_stream)), "wg_step")
+            for st in streams[1:]:
+                ev = torch.cuda.Event()
+                ev.record(st)
+                cur.wait_event(ev)
+
+        self._steps_at = -1
+        if not graph:
+            body(torch.cuda.current_stream(self.device))
+            return
+        g = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream(device=self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
+            with torch.cuda.graph(g, stream=side):
+                body(side)
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        g.replay()
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        self._policy_graph = g   # (kept until the next call: the replay may still be running)
+
     def graph(self, actions, n_steps: int, info: bool = True, lanes: Optional[int] = None):
         """Capture run(actions, n_steps) into a HIP graph (torch.cuda.CUDAGraph over the ROCm runtime) and
         return it as a WalkerGraph; replay() then advances the batch n_steps with one host call, the two walker

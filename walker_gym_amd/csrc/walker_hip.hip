@@ -76,6 +76,9 @@ struct KParams {
     int prio;         // WG_LEAN_PRIO: 1 (default) raise the wave priority while a lean tile issues its loads, so a
                       // wave's HBM requests leave before other waves' arithmetic; 0 off
     int xcd;          // WG_XCD bitmask: XCD-aware workgroup order (xcd_block) for 1 the wave kernel, 2 the lean kernel
+    int stagger;      // WG_STAGGER (experiment): cycles a first-round workgroup waits per dispatch slot before its loads
+    int stagger_cus;  // workgroups per dispatch slot (one per CU); slots 0 .. stagger_slots-1 are the first round
+    int stagger_slots;
 };
 
 // XCD-aware workgroup order: MI355X deals workgroups round-robin over its 8 XCDs (each with its own L2; observed
@@ -552,6 +555,8 @@ __device__ __forceinline__ void env_forces(const KParams &kp, float mf, float ym
         if (kp.neg_dampk != 0.f) emin = min(emin, fexp3(dvx, dvy, dvz));   // (a zero damping makes them zeros)
     }
     ax = ax + zm; ay = ay + fdiv_env<FAST>(kp.neg_g, mf, ymf); az = az + zm;
+    // (a wave-uniform dampk == 0 branch adding the signed-zero dividends directly, without their quotients, measured
+    // +40 VALU per wave and +0.5 % per launch: profiles/r04d_ab_canonical.json)
     ax = ax + fdiv_env<FAST>(dvx, mf, ymf);
     ay = ay + fdiv_env<FAST>(dvy, mf, ymf);
     az = az + fdiv_env<FAST>(dvz, mf, ymf);
@@ -573,12 +578,64 @@ __device__ __forceinline__ void env_forces(const KParams &kp, float mf, float ym
 #ifndef WG_FAST_ENV
 #define WG_FAST_ENV 1
 #endif
+#ifndef WG_ENV_PRE
+#define WG_ENV_PRE 1   // barrier-free kernels: the env-force quotients computed before the mass loop (EnvTerms)
+#endif
+// The env forces' quotients of one mass that do not depend on ground contact (gravity, damping), which depend on m and
+// v only: the barrier-free kernels compute them before the mass loop, so after it only their ordered additions and the
+// contact terms remain (env_apply: env_forces<true>'s additions in the same order, bit-identical).  (All nine quotients
+// ahead of the loop needed ten more registers across it: 32 B of scratch at the 6-wave budget.)
+struct EnvTerms {
+    float zm, eg, edx, edy, edz;   // 0/m, -g/m, the damping quotients
+    int emin;                      // least fexp over their dividends (the caller's exact-range test)
+};
+__device__ __forceinline__ EnvTerms env_terms(const KParams &kp, float mf, float ymf, float vx, float vy, float vz) {
+    EnvTerms e;
+    e.zm = fdiv_fast(0.f, mf, ymf);
+    const float dvx = kp.neg_dampk * vx, dvy = kp.neg_dampk * vy, dvz = kp.neg_dampk * vz;
+    e.emin = fexp(kp.neg_g);
+    if (kp.neg_dampk != 0.f) e.emin = min(e.emin, fexp3(dvx, dvy, dvz));
+    e.eg = fdiv_fast(kp.neg_g, mf, ymf);
+    e.edx = fdiv_fast(dvx, mf, ymf); e.edy = fdiv_fast(dvy, mf, ymf); e.edz = fdiv_fast(dvz, mf, ymf);
+    return e;
+}
+__device__ __forceinline__ void env_apply(const EnvTerms &e, const KParams &kp, float mf, float ymf, float vx, float vy,
+                                          float vz, float py, float &ax, float &ay, float &az, bool &hit, int &emin) {
+    emin = e.emin;
+    ax = ax + e.zm; ay = ay + e.eg; az = az + e.zm;
+    ax = ax + e.edx; ay = ay + e.edy; az = az + e.edz;
+    const float deep = py - kp.ground;
+    hit = deep < 0.f;                                                // optimized_env.py:154
+    if (hit) {
+        const float gk = kp.neg_groundk * deep, gd = kp.neg_grounddamp * vy;
+        ax = ax + e.zm; ay = ay + fdiv_fast(gk, mf, ymf); az = az + e.zm;
+        ax = ax + e.zm; ay = ay + fdiv_fast(gd, mf, ymf); az = az + e.zm;
+        const float ff = fabsf(deep) * kp.friction;                  // :168
+        const float fx = kp.friction_mode ? (vx * deep) * kp.friction : (-vx) * ff;
+        const float fz = kp.friction_mode ? (vz * deep) * kp.friction : (-vz) * ff;
+        emin = min(emin, min(fexp3(gk, gd, fx), fexp(fz)));
+        ax = ax + fdiv_fast(fx, mf, ymf); ay = ay + e.zm; az = az + fdiv_fast(fz, mf, ymf);
+    }
+}
+
 __device__ __forceinline__ void mass_tail(const KParams &kp, float mf, float ymf, const float *p3, const float *v3,
                                           float &px, float &py, float &pz, float &vx, float &vy, float &vz,
-                                          float &ax, float &ay, float &az, bool &hit, bool pinned) {
+                                          float &ax, float &ay, float &az, bool &hit, bool pinned,
+                                          const EnvTerms *pre = nullptr) {
     vx = v3[0]; vy = v3[1]; vz = v3[2];
     px = p3[0]; py = p3[1]; pz = p3[2];
-    if (WG_FAST_ENV) {
+    if (WG_ABLATE & 256) {   // (ablation: no env forces)
+        hit = py < kp.ground;
+    } else if (WG_FAST_ENV && pre) {
+        // the contact-free quotients came from env_terms before the mass loop
+        const float sx = ax, sy = ay, sz = az;
+        int emin = 0;
+        env_apply(*pre, kp, mf, ymf, vx, vy, vz, py, ax, ay, az, hit, emin);
+        if (__builtin_expect(!__builtin_isfinite(ax + ay + az) || ((WG_GUARDS & 4) && (emin < TINY_EXP || !divisor_ok(mf))), 0)) {
+            ax = sx; ay = sy; az = sz;
+            env_forces<false>(kp, mf, ymf, vx, vy, vz, py, ax, ay, az, hit, emin);
+        }
+    } else if (WG_FAST_ENV) {
         const float sx = ax, sy = ay, sz = az;
         int emin = 0;
         env_forces<true>(kp, mf, ymf, vx, vy, vz, py, ax, ay, az, hit, emin);
@@ -1672,6 +1729,9 @@ __device__ __forceinline__ float lane_gather(float v, int src_byte) {
 #ifndef WG_FAST_SPRING
 #define WG_FAST_SPRING 1
 #endif
+#ifndef WG_SPRING_CHK
+#define WG_SPRING_CHK 1   // the fast spring path's range test on nf instead of finiteness tests of every quotient
+#endif
 // Spring term and damping force of one edge from its endpoints' state (gathered from the mass lanes):
 // spring_edge's arithmetic with the cheaper reciprocal (identical results; cold path unchanged).
 // Cold path: every quantity again with IEEE divisions and numpy's sqrt (exact for every input).
@@ -1724,11 +1784,19 @@ __device__ __forceinline__ void spring_terms(const EdgeRec &e, float x, float pi
         t1 = ddiv_fast((double)(nf * r1), dist, yc);
         t2 = ddiv_fast((double)(nf * r2), dist, yc);
     }
-    // the quotients are exact when every one is finite; a non-finite one makes its sum non-finite (|d| <= 1
-    // cannot overflow a sum of three)
     bool rok = true;
     if ((WG_GUARDS & 1) && __builtin_expect(!pos_ok, 0)) rok = fexp3(r0, r1, r2) >= TINY_EXP;
+#if WG_SPRING_CHK
+    // mid holds only for finite differences with |r| < 2^20 (an inf / NaN / overflowing square fails it), so the d
+    // quotients are finite; |nf| < 2^100 (false for NaN) keeps nf * r below 2^120 and every t quotient finite and in
+    // Markstein's exact range (|t| in [2^-170, 2^140] or 0): the same lanes' quotients as the finiteness tests of
+    // d and t certified, with five fewer VALU (a larger |nf| now takes the exact cold path too: same results)
+    const bool fast_ok = mid && rok && __builtin_fabsf(nf) < 0x1p100f;
+#else
+    // the quotients are exact when every one is finite; a non-finite one makes its sum non-finite (|d| <= 1
+    // cannot overflow a sum of three)
     const bool fast_ok = mid && rok && __builtin_isfinite(d0 + d1 + d2) && __builtin_isfinite(t0 + t1 + t2);
+#endif
     if (__builtin_expect(!fast_ok, 0)) spring_terms_cold(e, x, r0, r1, r2, t0, t1, t2, d0, d1, d2, spring_mode);
 #else
     spring_terms_cold(e, x, r0, r1, r2, t0, t1, t2, d0, d1, d2, spring_mode);
@@ -2087,6 +2155,10 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
         const int bi = (ewl * M + edge_i(ij)) << 2, bj = (ewl * M + edge_j(ij)) << 2;
 #pragma unroll
         for (int c = 0; c < 3; c++) {
+            if (WG_ABLATE & 512) {   // (ablation: no gathers, the lane's own state at both ends, shifted)
+                g.v[c] = L.p3[c]; g.v[3 + c] = L.p3[c] + (float)(bj - bi); g.v[6 + c] = L.v3[c]; g.v[9 + c] = L.v3[c];
+                continue;
+            }
             g.v[c] = lane_gather(L.p3[c], bi); g.v[3 + c] = lane_gather(L.p3[c], bj);
             g.v[6 + c] = lane_gather(L.v3[c], bi); g.v[9 + c] = lane_gather(L.v3[c], bj);
         }
@@ -2126,6 +2198,11 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
     STAMP(3);
 
     // ================= masses: ordered accumulation, env forces, Point.run1 =================
+    // the env forces' quotients (m, v and y of the step's start only) ahead of the mass loop, once the spring records'
+    // registers are free: after the loop only their ordered additions remain (the resident kernel, whose state
+    // registers are tight, keeps them in mass_tail)
+    EnvTerms et{};
+    if (WG_ENV_PRE && !RES) et = env_terms(kp, mf, (float)ym, L.v3[0], L.v3[1], L.v3[2]);
     float px = 0.f, py = 0.f, pz = 0.f, vx = 0.f, vy = 0.f, vz = 0.f, ax = 0.f, ay = 0.f, az = 0.f;
     float nv = 0.f, ke = 0.f, pe = 0.f;
     bool hit = false;
@@ -2143,7 +2220,8 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
     // every lane (gathers); the resident kernel runs pair-free batches only (wg_rollout falls back to wg_step)
     if (!RES && kp.pair_mode) pair_forces(b, kp, L.p3, mf, pl, lane, M, is_mass, ax, ay, az);
     if (is_mass) {
-        mass_tail(kp, mf, (float)ym, L.p3, L.v3, px, py, pz, vx, vy, vz, ax, ay, az, hit, pin);
+        mass_tail(kp, mf, (float)ym, L.p3, L.v3, px, py, pz, vx, vy, vz, ax, ay, az, hit, pin,
+                  (WG_ENV_PRE && !RES) ? &et : nullptr);
         if (b.radius && store) b.radius[pl] = hit ? 3.0 : 1.0;   // p.r = 3 / p.r = 1 (gym/optimized_env.py:156,175)
         nv = np_norm3(vx, vy, vz);
         ke = mf * np_sq<NE == 1>(nv);   // p.m * norm(p.v) ** 2 (gym/optimized_env.py:242)
@@ -2153,7 +2231,8 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
 
     // ================= per-walker reductions (wave shuffles) + outputs (gym/optimized_env.py:189-248)
     const int gbase = lane & ~(M - 1);
-    const WalkerSums ws = walker_sums(px, py, pz, nv, ke, pe, gbase, M, lane);
+    const WalkerSums ws = (WG_ABLATE & 4) ? WalkerSums{px, py, pz, py, nv, ke, pe}   // (ablation: no reductions)
+                                          : walker_sums(px, py, pz, nv, ke, pe, gbase, M, lane);
     const float sx = ws.sx, sy = ws.sy, sz = ws.sz, ysum = ws.ysum, vsum = ws.vsum, ksum = ws.ksum, psum = ws.psum;
     const unsigned long long gmask = (M == 64) ? ~0ull : (((1ull << M) - 1ull) << gbase);
     const unsigned long long hb = __ballot(is_mass && (py - kp.ground < 0.f));   // contacts after run1 (:200)
@@ -2259,6 +2338,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lean_waves(
     STAMP(0);
     const LeanTile t = lean_tile_of(b, action, action_cols, lg, tile, lane);
     LeanIn<NE> L;
+    // (experiment) the first round of workgroups issues its loads slot by slot instead of all at once, so the first
+    // slot's data lands early and its arithmetic overlaps the later slots' loads
+    if (kp.stagger > 0) {
+        const int slot = (int)blockIdx.x / kp.stagger_cus;
+        if (slot > 0 && slot < kp.stagger_slots) {
+            const unsigned long long t0 = __builtin_amdgcn_s_memtime(), until = t0 + (unsigned long long)slot * kp.stagger;
+            while (__builtin_amdgcn_s_memtime() < until) __builtin_amdgcn_s_sleep(8);
+        }
+    }
     // load-phase wave priority: this wave's HBM requests leave before other waves' arithmetic
     if (kp.prio) __builtin_amdgcn_s_setprio(2);
     lean_load<NE>(b, kp, action, action_stride, t, lane, L);
@@ -2512,6 +2600,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
     STAMP(3);
 
     // ================= masses: ordered accumulation, env forces, Point.run1 =================
+    EnvTerms et{};
+    if (WG_ENV_PRE) et = env_terms(kp, mf, (float)ym, v3[0], v3[1], v3[2]);   // (as the lean kernel)
     float px = 0.f, py = 0.f, pz = 0.f, vx = 0.f, vy = 0.f, vz = 0.f, ax = 0.f, ay = 0.f, az = 0.f;
     bool hit = false;
     if (is_mass) {
@@ -2521,7 +2611,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
         else
             mass_accumulate<TermsAoS, true>(ts, reinterpret_cast<const uint16_t *>(s_inc) + 2 * mlb, mlb, io0, io1, mf,
                                             ax, ay, az, 0, wave_tiny);
-        mass_tail(kp, mf, (float)ym, p3, v3, px, py, pz, vx, vy, vz, ax, ay, az, hit, pin != 0);
+        mass_tail(kp, mf, (float)ym, p3, v3, px, py, pz, vx, vy, vz, ax, ay, az, hit, pin != 0,
+                  WG_ENV_PRE ? &et : nullptr);
         const uint32_t pl = (uint32_t)(P0 + lane);
         float *gpo = b.pos + 3 * (size_t)pl, *gvo = b.vel + 3 * (size_t)pl, *gao = b.acc + 3 * (size_t)pl;
         gpo[0] = px; gpo[1] = py; gpo[2] = pz;
@@ -2740,6 +2831,9 @@ KParams make_kparams(const wg_params &p) {
     k.friction_mode = p.friction_mode;
     k.prio = env_int("WG_LEAN_PRIO", 1);
     k.xcd = env_int("WG_XCD", 3);   // both kernels (profiles/r03e_ab_canon.json, r03d_ab_ragged_window_xcd.json)
+    k.stagger = env_int("WG_STAGGER", 0);
+    k.stagger_cus = env_int("WG_STAGGER_CUS", 256);
+    k.stagger_slots = env_int("WG_STAGGER_SLOTS", 6);
     k.dt2 = (float)(p.dt * p.dt);
     return k;
 }

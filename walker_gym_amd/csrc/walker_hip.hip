@@ -1729,6 +1729,9 @@ __device__ __forceinline__ float lane_gather(float v, int src_byte) {
 #ifndef WG_FAST_SPRING
 #define WG_FAST_SPRING 1
 #endif
+#ifndef WG_QMOVE
+#define WG_QMOVE 0   // A/B builds only: the lean kernel's quotients t/m and df/m formed once per
+#endif               // spring end in the edge phase (72 B of LDS per spring) instead of once per incidence entry
 #ifndef WG_SPRING_CHK
 #define WG_SPRING_CHK 1   // the fast spring path's range test on nf instead of finiteness tests of every quotient
 #endif
@@ -2172,13 +2175,53 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
         const bool mus = le < nE && ew < A;
         const float xs = s_x[mus ? ewl * A + ew : 0];
         const float xr = mus ? xs : e.rest;
+#if WG_QMOVE
+        // both ends' masses and reciprocals from the mass lanes (every lane takes part in the gathers)
+        const int ewl2 = fdiv(le, K, lg.invK);
+        const int qbi = (ewl2 * M + edge_i(e.ij)) << 2, qbj = (ewl2 * M + edge_j(e.ij)) << 2;
+        const float mi = lane_gather(mf, qbi), mj = lane_gather(mf, qbj);
+        const double ymi = lane_gather_d(ym, qbi), ymj = lane_gather_d(ym, qbj);
+#endif
         if (le < nE) {
             if (WG_ABLATE & 1) {   // profiling builds only: no spring arithmetic
                 ts.put(le, xr + g.v[0] + g.v[3] + g.v[6] + g.v[9], g.v[1] + g.v[4] + g.v[7] + g.v[10],
                        g.v[2] + g.v[5] + g.v[8] + g.v[11], e.k, e.c, 0.f);
             } else {
+#if WG_QMOVE
+              if (RES) {   // (the resident kernel is not part of the A/B: it keeps the per-entry quotients)
+                spring_edge_regs(e, le, xr, g.v[0], g.v[1], g.v[2], g.v[3], g.v[4], g.v[5], g.v[6], g.v[7], g.v[8],
+                                 g.v[9], g.v[10], g.v[11], ts, 0, gtiny, pos_ok);
+              } else {
+                double t0, t1, t2;
+                float g0, g1, g2;
+                spring_terms(e, xr, g.v[0], g.v[1], g.v[2], g.v[3], g.v[4], g.v[5], g.v[6], g.v[7], g.v[8], g.v[9],
+                             g.v[10], g.v[11], t0, t1, t2, g0, g1, g2, 0, pos_ok);
+                const double mdi = (double)mi, mdj = (double)mj;
+                const float ymfi = (float)ymi, ymfj = (float)ymj;
+                double qi0 = ddiv_fast(t0, mdi, ymi), qi1 = ddiv_fast(t1, mdi, ymi), qi2 = ddiv_fast(t2, mdi, ymi);
+                double qj0 = ddiv_fast(t0, mdj, ymj), qj1 = ddiv_fast(t1, mdj, ymj), qj2 = ddiv_fast(t2, mdj, ymj);
+                float di0 = fdiv_fast(g0, mi, ymfi), di1 = fdiv_fast(g1, mi, ymfi), di2 = fdiv_fast(g2, mi, ymfi);
+                float dj0 = fdiv_fast(g0, mj, ymfj), dj1 = fdiv_fast(g1, mj, ymfj), dj2 = fdiv_fast(g2, mj, ymfj);
+                // the mass loop's guards, per spring: a damping force below the f32 quotient's exact range, a mass
+                // outside its divisor range, or a non-finite quotient: this spring's quotients as IEEE divisions
+                const bool bad = fexp3(g0, g1, g2) < TINY_EXP || !divisor_ok(mi) || !divisor_ok(mj) ||
+                                 !__builtin_isfinite(((qi0 + qi1) + (qi2 + qj0)) + (qj1 + qj2)) ||
+                                 !__builtin_isfinite(((di0 + di1) + (di2 + dj0)) + (dj1 + dj2));
+                if (__builtin_expect(bad, 0)) {
+                    qi0 = t0 / mdi; qi1 = t1 / mdi; qi2 = t2 / mdi; qj0 = t0 / mdj; qj1 = t1 / mdj; qj2 = t2 / mdj;
+                    di0 = g0 / mi; di1 = g1 / mi; di2 = g2 / mi; dj0 = g0 / mj; dj1 = g1 / mj; dj2 = g2 / mj;
+                }
+                // record of spring le: [+t/m_i x3 | -t/m_j x3] f64, then [-df/m_i x3 | +df/m_j x3] f32: end i adds
+                // +t/m_i then -df/m_i, end j -t/m_j then +df/m_j (acc_entry_v2's signs, exact negations)
+                double *qr = reinterpret_cast<double *>(sl) + 9 * le;
+                qr[0] = qi0; qr[1] = qi1; qr[2] = qi2; qr[3] = -qj0; qr[4] = -qj1; qr[5] = -qj2;
+                float *dr = reinterpret_cast<float *>(qr + 6);
+                dr[0] = -di0; dr[1] = -di1; dr[2] = -di2; dr[3] = dj0; dr[4] = dj1; dr[5] = dj2;
+              }
+#else
                 spring_edge_regs(e, le, xr, g.v[0], g.v[1], g.v[2], g.v[3], g.v[4], g.v[5], g.v[6], g.v[7], g.v[8],
                                  g.v[9], g.v[10], g.v[11], ts, 0, gtiny, pos_ok);   // lean path: spring_mode 0 only
+#endif
             }
         }
     };
@@ -2210,7 +2253,19 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
         const int r1 = (WG_ABLATE & 2) ? min(L.io1, L.io0 + 1) : L.io1;
         const int lb = wl * K;
         // (the resident kernel keeps the XOR sign form: 5 fewer registers where its carried state is live)
-        if (WG_MASS_V2 && !RES)
+        if (WG_QMOVE && !RES) {
+            // quotient records (72 B per spring): end e of spring le at 72 le + 24 e (f64 x3) and 72 le + 48 + 12 e
+            const uint16_t *p = reinterpret_cast<const uint16_t *>(s_inc) + 2 * lb;
+            const char *base = sl + 72 * lb;
+            for (int r = L.io0; r < r1; r++) {
+                const uint32_t ent = p[r];
+                const char *rec = base + __umul24(ent >> 1, 72u);
+                const double *q = reinterpret_cast<const double *>(rec + 24 * (ent & 1u));
+                const float *dq = reinterpret_cast<const float *>(rec + 48 + 12 * (ent & 1u));
+                ax = (float)((double)ax + q[0]); ay = (float)((double)ay + q[1]); az = (float)((double)az + q[2]);
+                ax = ax + dq[0]; ay = ay + dq[1]; az = az + dq[2];
+            }
+        } else if (WG_MASS_V2 && !RES)
             mass_accumulate_v2(ts, reinterpret_cast<const uint16_t *>(s_inc) + 2 * lb, lb, L.io0, r1, mf, ym, ax, ay, az,
                                wave_tiny);
         else
@@ -2320,7 +2375,7 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
 
 // NE spring passes per wave need up to 8 x 16-B records in registers: 6 waves per SIMD hold up to NE 4 without
 // spills, NE 8 (up to 512 springs per 64 lanes) gets the 4-wave register budget.
-constexpr int lean_waves(int NE) { return NE >= 8 ? 4 : 6; }
+constexpr int lean_waves(int NE) { return WG_QMOVE ? 3 : NE >= 8 ? 4 : 6; }   // (QMOVE: its LDS allows 3 per SIMD)
 
 // One tile (64 / M walkers) per wave; waves never wait for one another.
 template <bool IN3D, int NE>
@@ -2590,8 +2645,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
         const bool mus = le < nE && ew < eA;
         const float xs = s_x[mus ? s_uo[ew_w] + ew : 0];
         const float xr = mus ? xs : e.rest;
-        if (le < nE)
-            spring_edge_regs(e, le, xr, pix, piy, piz, pjx, pjy, pjz, vix, viy, viz, vjx, vjy, vjz, ts, 0, gtiny, pos_ok);
+        if (le < nE) {
+            if (WG_ABLATE & 1)   // profiling builds only: no spring arithmetic
+                ts.put(le, xr + pix + pjx + vix + vjx, piy + pjy + viy + vjy, piz + pjz + viz + vjz, e.k, e.c, 0.f);
+            else
+                spring_edge_regs(e, le, xr, pix, piy, piz, pjx, pjy, pjz, vix, viy, viz, vjx, vjy, vjz, ts, 0, gtiny,
+                                 pos_ok);
+        }
     }
     wave_sync();
     // any spring of the wave with a damping force outside the exact range: every mass loop of the wave divides by m with
@@ -2606,8 +2666,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
     bool hit = false;
     if (is_mass) {
         if (WG_MASS_V2)
-            mass_accumulate_v2(ts, reinterpret_cast<const uint16_t *>(s_inc) + 2 * mlb, mlb, io0, io1, mf, ym, ax, ay, az,
-                               wave_tiny);
+            mass_accumulate_v2(ts, reinterpret_cast<const uint16_t *>(s_inc) + 2 * mlb, mlb, io0,
+                               (WG_ABLATE & 2) ? min(io1, io0 + 1) : io1, mf, ym, ax, ay, az, wave_tiny);
         else
             mass_accumulate<TermsAoS, true>(ts, reinterpret_cast<const uint16_t *>(s_inc) + 2 * mlb, mlb, io0, io1, mf,
                                             ax, ay, az, 0, wave_tiny);
@@ -2691,7 +2751,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
     // Walker w's row (the caller's row s_row[w]) is per*M_w values, the 3 conmid values, A_w muscle lengths, then
     // zeros to the stride.  Each mass lane stores its 3d values straight from registers as d-float pieces, each
     // muscle lane its length; the padding is written only when the caller's buffer is not known to be clean.
-    if (o.obs) {
+    if (o.obs && !(WG_ABLATE & 16)) {
         constexpr int d = IN3D ? 3 : 2, per = 3 * d;
         const int stride = o.obs_stride, nmid = kp.conmid ? 3 : 0;
         typedef float fvd __attribute__((ext_vector_type(d), aligned(4)));
@@ -2980,11 +3040,16 @@ bool lean_geo(const wg_batch *b, int obs_stride, LeanGeo *out, int spring_mode =
     const int ew = g.wpw * b->K;                          // springs of a full wave tile
     g.pl = (ew + 3) & ~3;                                 // spring-term slots: 16-B aligned regions
     // t (f64 x3) | df (f32 x3) | incidence words | x (observation rows go from registers to HBM, no LDS tile)
+#if WG_QMOVE
+    g.off_df = align16(g.pl * 72);                        // (quotient move: both ends' quotient records, no df)
+    g.off_inc = g.off_df;
+#else
     g.off_df = align16(g.pl * 24);
     g.off_inc = g.off_df + align16(g.pl * 12);
+#endif
     g.off_x = g.off_inc + align16(ew * 4 + 4);              // + the zero word after the last list (mass_accumulate_v2)
     g.slice = g.off_x + align16(std::max(1, g.wpw * b->A) * 4);
-    if (4 * g.slice > 80 * 1024) return false;
+    if (4 * g.slice > (WG_QMOVE ? 120 : 80) * 1024) return false;
     g.invK = 1.f / (float)b->K;
     g.invA = 1.f / (float)std::max(1, b->A);
     g.invM = 1.f / (float)M;

@@ -81,6 +81,22 @@ struct KParams {
     int stagger_slots;
 };
 
+// The per-step outputs the step kernels write: wg_outputs without the opt-in info pointers (walker_info_kernel writes
+// those), passed by value as a kernel argument.  (wg_outputs itself by value put its ABI-10 fields among the lean
+// kernel's arguments: 20 more SGPR spill instructions, v_writelane / v_readlane, and +16 VALU per wave.)
+struct KOut {
+    float *obs, *reward;
+    uint8_t *done;
+    float *centroid, *energy;
+    int32_t *steps;
+    int64_t obs_step, out_step;
+    int32_t obs_stride, obs_pad_clean;
+};
+inline KOut kout(const wg_outputs &o) {
+    return KOut{o.obs, o.reward, o.done, o.centroid, o.energy, o.steps, o.obs_step, o.out_step, o.obs_stride,
+                o.obs_pad_clean};
+}
+
 // XCD-aware workgroup order: MI355X deals workgroups round-robin over its 8 XCDs (each with its own L2; observed
 // placement, speed only), so hardware block b runs on XCD group b % 8.  The guide's bijective T1 swizzle maps b to a
 // logical block so that each XCD group takes one contiguous run of logical blocks, in launch order: consecutive
@@ -1283,7 +1299,7 @@ constexpr int wg_kernel_waves() { return (STEP && PWD == 0 && !SHFL && WG_WG_OCC
 template <bool STEP, bool RAGGED, bool IN3D, int PWD, bool SHFL>
 __global__ __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(wg_kernel_waves<STEP, RAGGED, IN3D, PWD, SHFL>()))) void walker_step_kernel(
     wg_batch b, KParams kp, const float *__restrict__ action, int action_cols, int action_stride,
-    wg_outputs o, const int32_t *__restrict__ plan, Geo geo) {
+    KOut o, const int32_t *__restrict__ plan, Geo geo) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     Carve s = carve(smem, geo);
     const int tid = threadIdx.x, lane = tid & 63, T = blockDim.x;
@@ -2104,7 +2120,7 @@ __device__ __forceinline__ LeanTerms lean_terms(char *sl, const LeanGeo &lg) {
 // edge in LDS, then each mass lane walks its incidence list, dividing by m as the reference does (mass_step).
 // RES (walker_rollout_lean): the tile's state stays in L across steps; it is written to HBM only when `last`.
 template <bool IN3D, int NE, bool RES = false>
-__device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &kp, const wg_outputs &o,
+__device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &kp, const KOut &o,
                                              const LeanGeo &lg, char *sl, const LeanTile &t, int lane,
                                              LeanIn<NE> &L, bool last = true) {
     const bool store = !RES || last;
@@ -2380,7 +2396,7 @@ constexpr int lean_waves(int NE) { return WG_QMOVE ? 3 : NE >= 8 ? 4 : 6; }   //
 // One tile (64 / M walkers) per wave; waves never wait for one another.
 template <bool IN3D, int NE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lean_waves(NE)))) void walker_step_lean(
-    wg_batch b, KParams kp, const float *__restrict__ action, int action_cols, int action_stride, wg_outputs o,
+    wg_batch b, KParams kp, const float *__restrict__ action, int action_cols, int action_stride, KOut o,
     LeanGeo lg) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -2421,7 +2437,7 @@ template <bool IN3D, int NE>
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4 : WG_RES_WAVES))) void walker_rollout_lean(
     wg_batch b, KParams kp, const float *__restrict__ action, int action_cols, int action_stride, int64_t action_step,
-    wg_outputs o, int n_steps, LeanGeo lg) {
+    KOut o, int n_steps, LeanGeo lg) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int tile = blockIdx.x * lg.wpb + wv;
@@ -2451,7 +2467,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
         if (ts.acts && s + 1 < n_steps)
             a_next = action[(size_t)(s + 1) * (size_t)action_step +
                             (size_t)(uint32_t)(ts.w0 + ts.mu_wl) * (uint32_t)action_stride + (uint32_t)ts.mu_ua];
-        wg_outputs os = o;
+        KOut os = o;
         if (os.obs) os.obs += (size_t)s * os.obs_step;
         if (os.reward) os.reward += (size_t)s * os.out_step;
         if (os.done) os.done += (size_t)s * os.out_step;
@@ -2492,7 +2508,7 @@ struct RagGeo {
 template <bool IN3D, int NE>
 // LDS: ~5.8 KB per wave at NE 2 (27 waves per CU); NE 4 / 8 tiles need more LDS and registers
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4 : NE >= 4 ? 5 : 6))) void walker_step_waves(
-    wg_batch b, KParams kp, const float *__restrict__ action, int action_cols, int action_stride, wg_outputs o,
+    wg_batch b, KParams kp, const float *__restrict__ action, int action_cols, int action_stride, KOut o,
     const int32_t *__restrict__ plan, int ntiles, RagGeo rg) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // the wave index as a wave-uniform (scalar) value: the plan entries and the tile's bases are then scalar loads
@@ -2974,7 +2990,7 @@ int launch(const wg_batch *b, const KParams &kp, const float *action, int cols, 
            const wg_outputs &o, const int32_t *plan, int blocks, const Geo &g, hipStream_t stream) {
     if (g.lds > LDS_LIMIT) return fail(WG_ERANGE, "workgroup needs %d B of LDS (> 160 KiB)", g.lds);
     hipLaunchKernelGGL((walker_step_kernel<STEP, RAGGED, IN3D, PWD, SHFL>), dim3(blocks), dim3(g.threads), g.lds, stream,
-                       *b, kp, action, cols, astride, o, plan, g);
+                       *b, kp, action, cols, astride, kout(o), plan, g);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(WG_EHIP, "launch failed: %s", hipGetErrorString(e));
     return 0;
@@ -3068,7 +3084,7 @@ int launch_lean(const wg_batch *b, const KParams &kp, bool in3d, const float *a,
     const int lds = g.wpb * g.slice + std::max(0, env_int("WG_LDS_PAD", 0));
 #define WG_LAUNCH_LEAN(D3, NE_)                                                                                  \
     hipLaunchKernelGGL((walker_step_lean<D3, NE_>), dim3(blocks), dim3(64 * g.wpb), lds, st, *b, kp, a, cols,   \
-                       astride, o, g)
+                       astride, kout(o), g)
 #define WG_LEAN_NE(D3)                                                         \
     do {                                                                       \
         if (ne <= 1) WG_LAUNCH_LEAN(D3, 1);                                    \
@@ -3092,7 +3108,7 @@ int launch_lean_rollout(const wg_batch *b, const KParams &kp, bool in3d, const f
     const int lds = g.wpb * g.slice;
 #define WG_LAUNCH_RO(D3, NE_)                                                                                    \
     hipLaunchKernelGGL((walker_rollout_lean<D3, NE_>), dim3(blocks), dim3(64 * g.wpb), lds, st, *b, kp, a, cols, \
-                       astride, astep, o, n_steps, g)
+                       astride, astep, kout(o), n_steps, g)
 #define WG_RO_NE(D3)                                                                                             \
     do {                                                                                                         \
         if (ne <= 1) WG_LAUNCH_RO(D3, 1);                                                                        \
@@ -3146,7 +3162,7 @@ int launch_waves(const wg_batch *b, const KParams &kp, bool in3d, const float *a
     const int lds = g.wpb * g.slice;
 #define WG_LAUNCH_WAVES(D3, NE_)                                                                                  \
     hipLaunchKernelGGL((walker_step_waves<D3, NE_>), dim3(blocks), dim3(64 * g.wpb), lds, st, *b, kp, a, cols,    \
-                       astride, o, plan, ntiles, g)
+                       astride, kout(o), plan, ntiles, g)
 #define WG_WAVES_NE(D3)                                                        \
     do {                                                                       \
         if (ne <= 1) WG_LAUNCH_WAVES(D3, 1);                                   \

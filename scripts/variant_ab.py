@@ -63,6 +63,9 @@ def time_one(lib, workload, steps=200, warm=20):
 def run(rounds, workload, env_specs=()):
     variants = [(f[4:-3], os.path.join(OUT, f), {}) for f in sorted(os.listdir(OUT)) if f.endswith(".so")] \
         if os.path.isdir(OUT) else []
+    only = [x for x in os.environ.get("WG_AB_ONLY", "").split(",") if x]   # a subset of the libraries by name
+    if only:
+        variants = [v for v in variants if v[0] in only]
     lib = os.path.join(ROOT, "walker_gym_amd", "libwalker_hip.so")
     for spec in env_specs:
         name, _, kv = spec.partition(":")

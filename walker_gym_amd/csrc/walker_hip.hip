@@ -76,9 +76,6 @@ struct KParams {
     int prio;         // WG_LEAN_PRIO: 1 (default) raise the wave priority while a lean tile issues its loads, so a
                       // wave's HBM requests leave before other waves' arithmetic; 0 off
     int xcd;          // WG_XCD bitmask: XCD-aware workgroup order (xcd_block) for 1 the wave kernel, 2 the lean kernel
-    int stagger;      // WG_STAGGER (experiment): cycles a first-round workgroup waits per dispatch slot before its loads
-    int stagger_cus;  // workgroups per dispatch slot (one per CU); slots 0 .. stagger_slots-1 are the first round
-    int stagger_slots;
 };
 
 // The per-step outputs the step kernels write: wg_outputs without the opt-in info pointers (walker_info_kernel writes
@@ -2409,15 +2406,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lean_waves(
     STAMP(0);
     const LeanTile t = lean_tile_of(b, action, action_cols, lg, tile, lane);
     LeanIn<NE> L;
-    // (experiment) the first round of workgroups issues its loads slot by slot instead of all at once, so the first
-    // slot's data lands early and its arithmetic overlaps the later slots' loads
-    if (kp.stagger > 0) {
-        const int slot = (int)blockIdx.x / kp.stagger_cus;
-        if (slot > 0 && slot < kp.stagger_slots) {
-            const unsigned long long t0 = __builtin_amdgcn_s_memtime(), until = t0 + (unsigned long long)slot * kp.stagger;
-            while (__builtin_amdgcn_s_memtime() < until) __builtin_amdgcn_s_sleep(8);
-        }
-    }
     // load-phase wave priority: this wave's HBM requests leave before other waves' arithmetic
     if (kp.prio) __builtin_amdgcn_s_setprio(2);
     lean_load<NE>(b, kp, action, action_stride, t, lane, L);
@@ -2585,7 +2573,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
         }
     }
     int wrow = w0 + lr, pin = 0;
-    if (b.row) wrow = at_u32(b.row, 4u * (w0 + lr));
+    if (b.row && !(WG_ABLATE & 2048)) wrow = at_u32(b.row, 4u * (w0 + lr));   // (ablation 2048: rows in stored order)
     if (b.pinned) pin = at_u32(b.pinned, (uint32_t)lp);
     // lane -> walker maps (tile-local offsets in LDS)
     if (lane <= nw) { s_mo[lane] = wmo; s_eo[lane] = weo; s_uo[lane] = wuo; }
@@ -2907,9 +2895,7 @@ KParams make_kparams(const wg_params &p) {
     k.friction_mode = p.friction_mode;
     k.prio = env_int("WG_LEAN_PRIO", 1);
     k.xcd = env_int("WG_XCD", 3);   // both kernels (profiles/r03e_ab_canon.json, r03d_ab_ragged_window_xcd.json)
-    k.stagger = env_int("WG_STAGGER", 0);
-    k.stagger_cus = env_int("WG_STAGGER_CUS", 256);
-    k.stagger_slots = env_int("WG_STAGGER_SLOTS", 6);
+
     k.dt2 = (float)(p.dt * p.dt);
     return k;
 }

@@ -69,6 +69,9 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline samples")
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--gather-to", choices=["root", "all"], default="root",
+                    help="rollout-end collective: root = dist.gather to rank 0 (the learner; each peer sends its block "
+                         "over its own link), all = all_gather into every rank")
     ap.add_argument("--gather", choices=["serial", "pipelined"], default="serial",
                     help="rollout-end observation gather inside the timed region: serial (default: this rollout's "
                          "final observations, after its last step) or pipelined (the previous rollout's, gathered "
@@ -350,10 +353,11 @@ def main():
     elif do_gather:
         # rollout-end gather (RCCL all_gather_into_tensor, shard sizes from shard_bounds): the final observations
         # [N, D] and, when recorded, every step's reward and done flags [K, N]
-        gathered = {"obs": gather_rollout(env.obs, n_total=world * N)}
+        dst = 0 if args.gather_to == "root" else None
+        gathered = {"obs": gather_rollout(env.obs, n_total=world * N, dst=dst)}
         if rec is not None:
-            gathered["reward"] = gather_rollout(rec["reward"], n_total=world * N, dim=1)
-            gathered["done"] = gather_rollout(rec["done"], n_total=world * N, dim=1)
+            gathered["reward"] = gather_rollout(rec["reward"], n_total=world * N, dim=1, dst=dst)
+            gathered["done"] = gather_rollout(rec["done"], n_total=world * N, dim=1, dst=dst)
     torch.cuda.synchronize()
     if in_world:
         dist.barrier()
@@ -371,20 +375,23 @@ def main():
         dist.barrier()
         torch.cuda.synchronize()
         tg = time.perf_counter()
-        gather_rollout(env.obs, n_total=world * N)
+        dst = 0 if (args.gather_to == "root" and prev_obs is None) else None
+        gather_rollout(env.obs, n_total=world * N, dst=dst)
         if rec is not None:
-            gather_rollout(rec["reward"], n_total=world * N, dim=1)
-            gather_rollout(rec["done"], n_total=world * N, dim=1)
+            gather_rollout(rec["reward"], n_total=world * N, dim=1, dst=dst)
+            gather_rollout(rec["done"], n_total=world * N, dim=1, dst=dst)
         torch.cuda.synchronize()
         tg_t = torch.tensor([time.perf_counter() - tg], dtype=torch.float64, device=dev)
         dist.all_reduce(tg_t, op=dist.ReduceOp.MAX)
         sent = {"obs": env.obs} if rec is None else {"obs": env.obs, "reward": rec["reward"], "done": rec["done"]}
-        gather_info = {"mode": args.gather, "rows": world * N, "tensors": sorted(gathered),
+        gather_info = {"mode": args.gather, "to": ("rank 0 (dist.gather)" if dst == 0 else "every rank (all_gather)"),
+                       "rows": world * N, "tensors": sorted(gathered),
                        "bytes_per_rank": int(sum(t.numel() * t.element_size() for t in sent.values())),
-                       "gathered_bytes": int(sum(t.numel() * t.element_size() for t in gathered.values())),
+                       "gathered_bytes": int(world * sum(t.numel() * t.element_size() for t in sent.values())),
                        "standalone_ms": round(float(tg_t.item()) * 1e3, 4),
                        "note": "serial (default): this rollout's final observations [N, D] and its per-step reward "
-                               "and done flags [K, N], after its last step, inside the timed region; pipelined "
+                               "and done flags [K, N], after its last step, inside the timed region, to rank 0 (the "
+                               "learner; --gather-to all: into every rank); pipelined "
                                "(opt-in): the previous rollout's final observations gathered while this rollout "
                                "steps; standalone_ms: the same gathers alone (max over ranks)"}
 

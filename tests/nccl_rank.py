@@ -41,6 +41,13 @@ def main(out_path: str) -> None:
             "device": str(g.device), "shape_ok": tuple(g.shape) == tuple(t.shape), "dtype_ok": g.dtype == t.dtype,
             "bitwise": bool(torch.equal(g.view(torch.uint8) if g.dtype != torch.uint8 else g,
                                         t.view(torch.uint8) if t.dtype != torch.uint8 else t))}
+    # the learner-only gather (dist.gather to rank 0, bench.py's default rollout-end collective)
+    for name, (t, nt) in {"root_final_obs": (env.obs, n), "root_reward_steps": (rew, n)}.items():
+        g = gather_rollout(t, n_total=nt, dim=1 if name == "root_reward_steps" else 0, dst=0)
+        torch.cuda.synchronize()
+        res["checks"][name] = {
+            "device": str(g.device), "shape_ok": tuple(g.shape) == tuple(t.shape), "dtype_ok": g.dtype == t.dtype,
+            "bitwise": bool(torch.equal(g.view(torch.uint8), t.contiguous().view(torch.uint8)))}
     # a wrong n_total is refused before any collective (shard_bounds disagrees with the local row count)
     try:
         gather_rollout(env.obs, n_total=n + 1)

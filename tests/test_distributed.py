@@ -51,6 +51,14 @@ def _worker(rank, world, port, n_total, T, out_q, by_size, pipelined=False):
     # the per-step records of SURVEY §8(e) ([T, n_r] -> [T, N], dim 1), as bench.py's rollout gather sends them
     rew_full = gather_rollout(torch.from_numpy(np.stack(rew)), n_total=None if by_size else n_total, dim=1)
     done_full = gather_rollout(torch.from_numpy(np.stack(done)), n_total=None if by_size else n_total, dim=1)
+    # the learner-only form (dist.gather to one rank; bench.py's default): the last rank receives, the others get None
+    root = world - 1
+    obs_root = gather_rollout(torch.from_numpy(obs), n_total=None if by_size else n_total, dst=root)
+    rew_root = gather_rollout(torch.from_numpy(np.stack(rew)), n_total=None if by_size else n_total, dim=1, dst=root)
+    if rank != root:
+        assert obs_root is None and rew_root is None
+    else:
+        assert np.array_equal(obs_root.numpy(), full.numpy()) and np.array_equal(rew_root.numpy(), rew_full.numpy())
     if rank == 0:
         out_q.put((full.numpy(), rew_full.numpy(), done_full.numpy()))
     dist.barrier()

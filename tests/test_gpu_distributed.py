@@ -81,7 +81,7 @@ def test_rccl_one_rank_gather_rollout_on_device(tmp_path):
     res = json.load(open(out))
     assert res["backend"] == "nccl" and res["world"] == 1
     assert res["wrong_n_total_refused"]
-    assert len(res["checks"]) == 6
+    assert len(res["checks"]) == 8
     for name, c in res["checks"].items():
         assert c["device"].startswith("cuda"), name
         assert c["shape_ok"] and c["dtype_ok"] and c["bitwise"], (name, c)

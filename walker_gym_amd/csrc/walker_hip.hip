@@ -2515,6 +2515,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
     float *s_x = reinterpret_cast<float *>(sl + rg.off_x);
     int *s_mo = reinterpret_cast<int *>(sl + rg.off_wo);              // [RW_MAXW + 1] tile-local offsets
     int *s_eo = s_mo + (RW_MAXW + 1), *s_uo = s_eo + (RW_MAXW + 1), *s_row = s_uo + (RW_MAXW + 1);
+    float *s_mid = reinterpret_cast<float *>(s_row + RW_MAXW);          // [RW_MAXW * 3] each walker's mean position
     // after the mass loop: per-mass terms in the spring-term region, pos [64*3] | |v| | m|v|^2 | m g (y-ground),
     // then the obs staging; the walker partials [RW_MAXW * 8] in the damping region
     float *s_tp = reinterpret_cast<float *>(sl);
@@ -2594,7 +2595,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
     if (!is_mass) mw = 0;
     if (!is_mus) uw = 0;
     wave_sync();
-    const int mlm = s_mo[mw], mM = s_mo[mw + 1] - mlm, mlb = s_eo[mw];
+    const int mlm = s_mo[mw], mlb = s_eo[mw];
     // inc_off (M_w + 1 entries per walker) and the action: the second (and last) round of vector loads
     const uint32_t io = (uint32_t)lp + (uint32_t)(w0 + mw);
     int io0 = at_u32(b.inc_off, 2u * io), io1 = at_u32(b.inc_off, 2u * io + 2u);
@@ -2743,12 +2744,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
             if (!done && steps > 100) done = all;
             o.done[wrow] = (uint8_t)done;
         }
-        if (o.centroid) {
-            o.centroid[3 * wrow] = fdiv_count(rd[0], fM, yM); o.centroid[3 * wrow + 1] = fdiv_count(rd[1], fM, yM);
-            o.centroid[3 * wrow + 2] = fdiv_count(rd[2], fM, yM);
-        }
+        // the walker's mean position (np.mean: info's centroid, getstat's mid), once per walker: every mass lane of the
+        // observation rows reads it from LDS instead of dividing again (-25 VALU per wave)
+        const float mx = fdiv_count(rd[0], fM, yM), my = fdiv_count(rd[1], fM, yM), mz = fdiv_count(rd[2], fM, yM);
+        s_mid[3 * lane] = mx; s_mid[3 * lane + 1] = my; s_mid[3 * lane + 2] = mz;
+        if (o.centroid) { o.centroid[3 * wrow] = mx; o.centroid[3 * wrow + 1] = my; o.centroid[3 * wrow + 2] = mz; }
         if (o.energy) o.energy[wrow] = 0.5f * rd[5] + rd[6];
     }
+    wave_sync();
     STAMP(5);
 
     // ================= observation rows: Creature.getstat (gym/optimized_walker.py:129-162) =========
@@ -2760,15 +2763,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
         const int stride = o.obs_stride, nmid = kp.conmid ? 3 : 0;
         typedef float fvd __attribute__((ext_vector_type(d), aligned(4)));
         if (is_mass) {
-            const float *rd = s_red + 8 * mw;
-            const float fM = (float)mM;
-            const double yM = rcp64_nr((double)mM);
+            const float *rd = kp.midform == 2 ? s_red + 8 * mw : s_mid + 3 * mw;   // G1 getstat: the SUM; else the mean
             float *dst = o.obs + (size_t)s_row[mw] * stride + per * (lane - mlm);
             const float pm[3] = {px, py, pz}, vm[3] = {vx, vy, vz}, am[3] = {ax, ay, az};
             fvd vp, vv, va;
 #pragma unroll
             for (int c = 0; c < d; c++) {
-                const float mid = kp.midform == 2 ? rd[c] : fdiv_count(rd[c], fM, yM);   // G1 getstat: the SUM
+                const float mid = rd[c];
                 vp[c] = kp.midform ? (pm[c] - mid) * kp.pk : pm[c] * kp.pk;
                 vv[c] = vm[c] * kp.vk;
                 va[c] = am[c] * kp.ak;
@@ -3136,7 +3137,7 @@ bool rag_geo(const wg_batch *b, int obs_stride, RagGeo *out) {
     g.off_inc = g.off_df + align16(std::max(ec * 12, 4 * RW_MAXW * 8));
     g.off_x = g.off_inc + align16(ec * 4 + 4);                   // + the read-ahead pad word (mass_accumulate_v2)
     g.off_wo = g.off_x + align16(64 * 4);
-    g.slice = g.off_wo + align16(4 * (RW_MAXW + 1) * 3 + 4 * RW_MAXW);
+    g.slice = g.off_wo + align16(4 * (RW_MAXW + 1) * 3 + 4 * RW_MAXW + 12 * RW_MAXW);   // + the walkers' means
     *out = g;
     return true;
 }

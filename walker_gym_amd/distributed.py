@@ -58,11 +58,13 @@ class GatherHandle:
         self._work, self._out, self._sizes, self._nmax, self._world = work, out, sizes, nmax, world
         self._dim = dim
 
-    def wait(self) -> torch.Tensor:
+    def wait(self) -> Optional[torch.Tensor]:
         if self._work is not None:
             self._work.wait()
             self._work = None
         out, sizes, nmax, world = self._out, self._sizes, self._nmax, self._world
+        if out is None:      # a gather to another rank: nothing lands here
+            return None
         if self._dim == 1:   # [world * T, nmax, ...] rank blocks -> [T, sum(sizes), ...] (one device copy)
             T = out.shape[0] // world
             blk = out.view((world, T) + tuple(out.shape[1:]))
@@ -75,7 +77,7 @@ class GatherHandle:
 
 
 def gather_rollout_async(local: torch.Tensor, group: Optional[dist.ProcessGroup] = None,
-                         n_total: Optional[int] = None, dim: int = 0) -> GatherHandle:
+                         n_total: Optional[int] = None, dim: int = 0, dst: Optional[int] = None) -> GatherHandle:
     """Issue the rollout-end gather (every rank's [n_r, ...] block concatenated along dim 0 in rank order) without
     waiting for it: on RCCL the collective runs on the process group's own stream, ordered after the work already
     queued on the calling stream, so steps issued afterwards overlap it (an actor loop gathers rollout i while
@@ -87,7 +89,12 @@ def gather_rollout_async(local: torch.Tensor, group: Optional[dist.ProcessGroup]
     all_gather of every rank's length.
 
     dim = 1: `local` is a per-step record [T, n_r, ...] (rewards, done flags); the rank blocks are gathered whole
-    (each rank's [T, nmax, ...] is one contiguous send buffer, no transpose copy) and returned as [T, N, ...]."""
+    (each rank's [T, nmax, ...] is one contiguous send buffer, no transpose copy) and returned as [T, N, ...].
+
+    dst = None: every rank receives the whole rollout (all_gather).  dst = r: only rank r — the learner of an
+    actor / learner split — receives it (dist.gather: every other rank sends its block straight to r, over its own xGMI
+    link on an 8-GPU node, instead of relaying the other ranks' blocks around a ring); the others' wait() returns
+    None."""
     if dim not in (0, 1):
         raise ValueError("dim must be 0 (walker rows) or 1 ([T, walkers, ...] records)")
     world = dist.get_world_size(group)
@@ -109,6 +116,17 @@ def gather_rollout_async(local: torch.Tensor, group: Optional[dist.ProcessGroup]
         pad[dim] = nmax - n
         block = torch.cat([block, block.new_zeros(pad)], dim)
     lead = block.shape[0]
+    if dst is not None:
+        if not 0 <= dst < world:
+            raise ValueError(f"dst {dst} is not a rank of this group (world {world})")
+        g_dst = dist.get_global_rank(group, dst) if group is not None else dst
+        out = (torch.empty((world * lead,) + tuple(block.shape[1:]), dtype=local.dtype, device=local.device)
+               if rank == dst else None)
+        work = dist.gather(block, list(out.chunk(world, 0)) if out is not None else None, dst=g_dst, group=group,
+                           async_op=True)
+        h = GatherHandle(work, out, sizes, nmax, world, dim)
+        h._block = block
+        return h
     out = torch.empty((world * lead,) + tuple(block.shape[1:]), dtype=local.dtype, device=local.device)
     if dist.get_backend(group) == "nccl":
         work = dist.all_gather_into_tensor(out, block, group=group, async_op=True)
@@ -120,7 +138,7 @@ def gather_rollout_async(local: torch.Tensor, group: Optional[dist.ProcessGroup]
 
 
 def gather_rollout(local: torch.Tensor, group: Optional[dist.ProcessGroup] = None,
-                   n_total: Optional[int] = None, dim: int = 0) -> torch.Tensor:
+                   n_total: Optional[int] = None, dim: int = 0, dst: Optional[int] = None) -> Optional[torch.Tensor]:
     """Concatenate every rank's block along the walker axis `dim`, in rank order — the rollout-end gather
-    (gather_rollout_async, waited for at once)."""
-    return gather_rollout_async(local, group, n_total, dim).wait()
+    (gather_rollout_async, waited for at once); with dst, on rank dst only (None elsewhere)."""
+    return gather_rollout_async(local, group, n_total, dim, dst).wait()

@@ -69,9 +69,9 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline samples")
     ap.add_argument("--no-gather", action="store_true")
-    ap.add_argument("--gather-to", choices=["root", "all"], default="root",
-                    help="rollout-end collective: root = dist.gather to rank 0 (the learner; each peer sends its block "
-                         "over its own link), all = all_gather into every rank")
+    ap.add_argument("--gather-to", choices=["root", "all"], default="all",
+                    help="rollout-end collective: all = all_gather_into_tensor into every rank (RCCL's ring "
+                         "collective); root = dist.gather to rank 0 (the learner; peer-to-peer sends)")
     ap.add_argument("--gather", choices=["serial", "pipelined"], default="serial",
                     help="rollout-end observation gather inside the timed region: serial (default: this rollout's "
                          "final observations, after its last step) or pipelined (the previous rollout's, gathered "
@@ -390,8 +390,8 @@ def main():
                        "gathered_bytes": int(world * sum(t.numel() * t.element_size() for t in sent.values())),
                        "standalone_ms": round(float(tg_t.item()) * 1e3, 4),
                        "note": "serial (default): this rollout's final observations [N, D] and its per-step reward "
-                               "and done flags [K, N], after its last step, inside the timed region, to rank 0 (the "
-                               "learner; --gather-to all: into every rank); pipelined "
+                               "and done flags [K, N], after its last step, inside the timed region, into every rank "
+                               "(--gather-to root: to rank 0 only); pipelined "
                                "(opt-in): the previous rollout's final observations gathered while this rollout "
                                "steps; standalone_ms: the same gathers alone (max over ranks)"}
 

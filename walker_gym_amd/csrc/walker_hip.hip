@@ -373,6 +373,25 @@ __device__ __forceinline__ double rcp64_nr(double d) {
     return __builtin_fma(y, e, y);
 }
 
+// RN64(1/m) of a mass: for m in the divisor range (divisor_ok: the only masses whose fast quotients are used) v_rcp_f64
+// and two Newton steps give the correctly rounded reciprocal — Markstein's correction from a y within one ulp is exact
+// unless m's 53-bit significand is all ones, which a float32 cannot have; checked on the GPU for every float32 in
+// the range, both signs (scripts/check_rcp64.hip, profiles/r04_rcp64_exhaustive.json) — 5 VALU instead of the ~12 of
+// the IEEE division, and a shorter dependent chain; any other m (0, subnormal, inf, NaN, outside the range) takes the
+// IEEE division, so the guarded paths see exactly what they saw before.
+#ifndef WG_YM_RCP
+#define WG_YM_RCP 1
+#endif
+__device__ __forceinline__ double rcp64_nr(double d);
+__device__ __forceinline__ bool divisor_ok(float m);
+__device__ __forceinline__ double recip_m(float mf) {
+    const double md = (double)mf;
+    if (!WG_YM_RCP) return 1.0 / md;
+    double y = rcp64_nr(md);
+    if (__builtin_expect(!divisor_ok(mf), 0)) y = 1.0 / md;
+    return y;
+}
+
 // numpy's float32 x / M for a walker's mass count M (np.mean's final division; 1 <= M < 2^20):
 // (float)(x * y) with y = rcp64_nr(M) (within about an ulp of 1/M).  When x / M is a normal float, it is either
 // representable or at least 2^-25 / M (relative) from every float rounding midpoint (a midpoint has a 25-bit odd
@@ -2151,7 +2170,7 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
         if (store) b.muscle_x[ul] = x;
     }
     if (is_mus) s_x[lane] = x;
-    double ym = 1.0 / (double)mf;   // IEEE 1/m of this lane's mass: every /m below is exact from it
+    double ym = recip_m(mf);        // RN64(1/m) of this lane's mass: every /m below is exact from it
     // (opaque: otherwise the compiler turns (float)ym, which is RN32(1/m), into a second, float32 IEEE division)
     if (WG_MASS_V2 && !RES) asm volatile("" : "+v"(ym));
     wave_sync();
@@ -2627,7 +2646,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
         b.muscle_x[U0 + lane] = x;
     }
     if (is_mus) s_x[lane] = x;
-    double ym = 1.0 / (double)mf;
+    double ym = recip_m(mf);
     if (WG_MASS_V2) asm volatile("" : "+v"(ym));   // (float)ym stays a conversion, not a float32 division
     wave_sync();
     STAMP(2);

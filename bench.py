@@ -588,6 +588,9 @@ def main():
             line["floor"] = {"empty_launch_us": fl[0], "load_store_launch_us": fl[1],
                              "step_over_load_store": round(step_ms * 1e3 / fl[1], 3),
                              "kernel_over_load_store": round(head_ms * 1e3 / fl[1], 3),
+                             # --resident: the same steps as one wg_rollout launch (no launch per step)
+                             **({"resident_step_over_load_store": round(resident_ms * 1e3 / fl[1], 3)}
+                                if resident_ms is not None else {}),
                              "grid": [geo["blocks"], geo["threads"]],
                              "source": "wg_launch_floor on this box (the step's grid, 2,000 back-to-back launches "
                                        "each, HIP events on the bench stream); scripts/launch_floor.hip is the "

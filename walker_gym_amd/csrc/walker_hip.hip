@@ -1906,6 +1906,19 @@ __device__ __forceinline__ const T &at_u32(const T *base, uint32_t byte_off) {
     const size_t off = WG_LEAN_CLAMP ? (size_t)byte_off : (size_t)(int64_t)(int32_t)byte_off;
     return *reinterpret_cast<const T *>(reinterpret_cast<const char *>(base) + off);
 }
+// The same form for the stores (global_store's saddr form): the lean and wave kernels' outputs, whose byte offsets the
+// host bounds below 4 GiB (u32_bytes, obs_u32).  WG_ST_U32=0 (A/B builds only) keeps the 64-bit element addressing.
+#ifndef WG_ST_U32
+#define WG_ST_U32 1
+#endif
+template <typename T>
+__device__ __forceinline__ T &at_u32w(T *base, uint32_t byte_off) {
+    return *reinterpret_cast<T *>(reinterpret_cast<char *>(base) + (size_t)byte_off);
+}
+// a walker's (or mass's) element e of a record of n floats: 64-bit element arithmetic, or the 32-bit byte offset
+#define WG_ST(base, e, n) (WG_ST_U32 ? &at_u32w((base), (uint32_t)(n) * 4u * (uint32_t)(e)) : (base) + (size_t)(n) * (size_t)(e))
+// a count (<= 64) halved and negated as the reference's float64 product: exact in float32 (-0.0 for 0, as -(0.0) * 0.5)
+__device__ __forceinline__ float neg_half_count(int n) { return -0.5f * (float)n; }
 template <int NE>
 __device__ __forceinline__ void lean_load_mass(const wg_batch &b, const LeanTile &t, int lane, LeanIn<NE> &L) {
     L.mf = 0.f; L.io0 = 0; L.io1 = 0; L.wsteps = 0; L.pin = 0;
@@ -2167,7 +2180,7 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
         x = (kp.action_mode == 1) ? ((L.a != 0.f) ? x + L.stp : x - L.stp) : x + L.a;
         if (L.lo > x) x = L.lo;     // Python max(x, originx*minl)
         if (L.hi < x) x = L.hi;     // Python min(x, originx*maxl)
-        if (store) b.muscle_x[ul] = x;
+        if (store) *WG_ST(b.muscle_x, ul, 1) = x;
     }
     if (is_mus) s_x[lane] = x;
     double ym = recip_m(mf);        // RN64(1/m) of this lane's mass: every /m below is exact from it
@@ -2187,7 +2200,8 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
         const int le = lane + 64 * it;
         const int ewl = fdiv(le, K, lg.invK);
         const uint32_t ij = L.er[it].ij;
-        const int bi = (ewl * M + edge_i(ij)) << 2, bj = (ewl * M + edge_j(ij)) << 2;
+        // (M | 64 is a power of two: the walker's first lane is a shift; 24-bit products below, one VALU each)
+        const int bi = ((ewl << lg.lgM) + edge_i(ij)) << 2, bj = ((ewl << lg.lgM) + edge_j(ij)) << 2;
 #pragma unroll
         for (int c = 0; c < 3; c++) {
             if (WG_ABLATE & 512) {   // (ablation: no gathers, the lane's own state at both ends, shifted)
@@ -2201,11 +2215,11 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
     auto spring = [&](int it, const Gath &g) {
         const int le = lane + 64 * it;
         const EdgeRec e = L.er[it];
-        const int ewl = fdiv(le, K, lg.invK), ew = le - ewl * K;
+        const int ewl = fdiv(le, K, lg.invK), ew = le - (int)__umul24(ewl, K);
         // the muscle's rest length read unconditionally (clamped index), then selected by value: a select
         // between the LDS slot and e.rest became a pointer select (flat load from a stack copy of e)
         const bool mus = le < nE && ew < A;
-        const float xs = s_x[mus ? ewl * A + ew : 0];
+        const float xs = s_x[mus ? (int)__umul24(ewl, A) + ew : 0];
         const float xr = mus ? xs : e.rest;
 #if WG_QMOVE
         // both ends' masses and reciprocals from the mass lanes (every lane takes part in the gathers)
@@ -2328,31 +2342,34 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
     const float midx = sx * lg.invM, midy = sy * lg.invM, midz = sz * lg.invM;
     if (is_mass) {
         if (store) {
-            float *gpo = b.pos + 3 * (size_t)pl, *gvo = b.vel + 3 * (size_t)pl, *gao = b.acc + 3 * (size_t)pl;
+            float *gpo = WG_ST(b.pos, pl, 3), *gvo = WG_ST(b.vel, pl, 3), *gao = WG_ST(b.acc, pl, 3);
             gpo[0] = px; gpo[1] = py; gpo[2] = pz;
             gvo[0] = vx; gvo[1] = vy; gvo[2] = vz;
             gao[0] = ax; gao[1] = ay; gao[2] = az;
-            if (b.contact) b.contact[pl] = (uint8_t)hit;
+            if (b.contact) at_u32w(b.contact, pl) = (uint8_t)hit;
         }
         if (q == 0) {
             const uint32_t wg = (uint32_t)(w0 + wl);
             const int steps = L.wsteps + 1;
-            if (store) b.steps[wg] = steps;
+            if (store) *WG_ST(b.steps, wg, 1) = steps;
             if (RES) L.wsteps = steps;
-            if (o.steps) o.steps[wg] = steps;
+            if (o.steps) *WG_ST(o.steps, wg, 1) = steps;
             const float cy = ysum * lg.invM;
             if (o.reward) {
                 const float vpen = (-(vsum * lg.invM)) * 0.1f;
-                o.reward[wg] = (cy + vpen) + (float)(-(double)__popcll(hb & gmask) * 0.5);
+                *WG_ST(o.reward, wg, 1) = (cy + vpen) + neg_half_count((int)__popcll(hb & gmask));
             }
             if (o.done) {
                 int done = steps >= kp.max_steps;
                 if (!done && cy < kp.done_y) done = 1;
                 if (!done && steps > 100) done = (sb & gmask) == gmask;
-                o.done[wg] = (uint8_t)done;
+                at_u32w(o.done, wg) = (uint8_t)done;
             }
-            if (o.centroid) { o.centroid[3 * wg] = midx; o.centroid[3 * wg + 1] = midy; o.centroid[3 * wg + 2] = midz; }
-            if (o.energy) o.energy[wg] = 0.5f * ksum + psum;
+            if (o.centroid) {
+                float *c = WG_ST(o.centroid, wg, 3);
+                c[0] = midx; c[1] = midy; c[2] = midz;
+            }
+            if (o.energy) *WG_ST(o.energy, wg, 1) = 0.5f * ksum + psum;
         }
     }
 
@@ -2365,7 +2382,7 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
         const int stride = o.obs_stride, nmid = kp.conmid ? 3 : 0;
         typedef float fvd __attribute__((ext_vector_type(d), aligned(4)));
         if (is_mass) {
-            float *wrow = o.obs + (uint32_t)(w0 + wl) * (uint32_t)stride;
+            const uint32_t row0 = (uint32_t)(w0 + wl) * (uint32_t)stride;   // the row's first element
             // G1 getstat (midform 2, gym/walker.py:88-96) subtracts the SUM of positions
             const float mm[3] = {kp.midform == 2 ? sx : midx, kp.midform == 2 ? sy : midy, kp.midform == 2 ? sz : midz};
             const float pm[3] = {px, py, pz}, vm[3] = {vx, vy, vz}, am[3] = {ax, ay, az};
@@ -2376,19 +2393,20 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
                 vv[c] = vm[c] * kp.vk;
                 va[c] = am[c] * kp.ak;
             }
-            float *dst = wrow + per * q;   // (a 3-vector's type is 16 B: no array indexing over fvd)
+            float *dst = WG_ST(o.obs, row0 + per * q, 1);   // (a 3-vector's type is 16 B: no array indexing over fvd)
             *reinterpret_cast<fvd *>(dst) = vp;
             *reinterpret_cast<fvd *>(dst + d) = vv;
             *reinterpret_cast<fvd *>(dst + 2 * d) = va;
             if (q == 0) {
                 if (nmid) {
-                    wrow[per * M] = kp.midform ? mm[0] : 0.f; wrow[per * M + 1] = kp.midform ? mm[1] : 0.f;
-                    wrow[per * M + 2] = kp.midform ? mm[2] : 0.f;
+                    float *mrow = WG_ST(o.obs, row0 + per * M, 1);
+                    mrow[0] = kp.midform ? mm[0] : 0.f; mrow[1] = kp.midform ? mm[1] : 0.f;
+                    mrow[2] = kp.midform ? mm[2] : 0.f;
                 }
-                for (int r = per * M + nmid + A; r < stride; r++) wrow[r] = 0.f;
+                for (int r = per * M + nmid + A; r < stride; r++) *WG_ST(o.obs, row0 + r, 1) = 0.f;
             }
         }
-        if (is_mus) o.obs[(uint32_t)(w0 + mu_wl) * (uint32_t)stride + per * M + nmid + mu_ua] = x * kp.mk;
+        if (is_mus) *WG_ST(o.obs, (uint32_t)(w0 + mu_wl) * (uint32_t)stride + per * M + nmid + mu_ua, 1) = x * kp.mk;
     }
     if (RES) {   // the next step starts from this one's state (Point.pos/v, Muscle.x), in registers
         L.p3[0] = px; L.p3[1] = py; L.p3[2] = pz;
@@ -2415,7 +2433,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lean_waves(
     wg_batch b, KParams kp, const float *__restrict__ action, int action_cols, int action_stride, KOut o,
     LeanGeo lg) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    // the wave index as a wave-uniform (scalar) value: the tile's walker range and element bases are then SALU
+    // products, not per-lane v_mul_lo_u32
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int blk = (kp.xcd & 2) ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     const int tile = blk * lg.wpb + wv;
     if (tile * lg.wpw >= b.N) return;
@@ -2440,13 +2460,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lean_waves(
 // walker_step_lean, step for step (bit-identical to n_steps single-step launches).
 template <bool IN3D, int NE>
 #ifndef WG_RES_WAVES
-#define WG_RES_WAVES 4   // waves per SIMD the resident kernel's register budget targets (its state stays live)
-#endif
+#define WG_RES_WAVES 5   // waves per SIMD the resident kernel's register budget targets (its state stays live):
+#endif                   // 5 since the scalar wave index (16 B of scratch at NE 3-4): 35.49 against 36.07 us per step
+                         // at 4 (profiles/r04l_ab_resident.json)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4 : WG_RES_WAVES))) void walker_rollout_lean(
     wg_batch b, KParams kp, const float *__restrict__ action, int action_cols, int action_stride, int64_t action_step,
     KOut o, int n_steps, LeanGeo lg) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int tile = blockIdx.x * lg.wpb + wv;
     if (tile * lg.wpw >= b.N) return;
 #ifdef WG_STAMPS
@@ -2643,7 +2664,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
         x = (kp.action_mode == 1) ? ((act != 0.f) ? x + mst : x - mst) : x + act;
         if (mlo > x) x = mlo;     // Python max(x, originx*minl)
         if (mhi < x) x = mhi;     // Python min(x, originx*maxl)
-        b.muscle_x[U0 + lane] = x;
+        *WG_ST(b.muscle_x, U0 + lane, 1) = x;
     }
     if (is_mus) s_x[lane] = x;
     double ym = recip_m(mf);
@@ -2698,11 +2719,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
         mass_tail(kp, mf, (float)ym, p3, v3, px, py, pz, vx, vy, vz, ax, ay, az, hit, pin != 0,
                   WG_ENV_PRE ? &et : nullptr);
         const uint32_t pl = (uint32_t)(P0 + lane);
-        float *gpo = b.pos + 3 * (size_t)pl, *gvo = b.vel + 3 * (size_t)pl, *gao = b.acc + 3 * (size_t)pl;
+        float *gpo = WG_ST(b.pos, pl, 3), *gvo = WG_ST(b.vel, pl, 3), *gao = WG_ST(b.acc, pl, 3);
         gpo[0] = px; gpo[1] = py; gpo[2] = pz;
         gvo[0] = vx; gvo[1] = vy; gvo[2] = vz;
         gao[0] = ax; gao[1] = ay; gao[2] = az;
-        if (b.contact) b.contact[pl] = (uint8_t)hit;
+        if (b.contact) at_u32w(b.contact, pl) = (uint8_t)hit;
         if (b.radius) b.radius[pl] = hit ? 3.0 : 1.0;   // gym/optimized_env.py:156,175
     }
     STAMP(4);
@@ -2754,21 +2775,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
         const int packed = __float_as_int(rd[7]);
         const int hits = packed >> 1, all = packed & 1;
         const int steps = wsteps + 1;
-        b.steps[w0 + lane] = steps;
-        if (o.steps) o.steps[wrow] = steps;
-        if (o.reward) o.reward[wrow] = (cy + (-fdiv_count(rd[4], fM, yM)) * 0.1f) + (float)(-(double)hits * 0.5);
+        *WG_ST(b.steps, w0 + lane, 1) = steps;
+        if (o.steps) *WG_ST(o.steps, wrow, 1) = steps;
+        if (o.reward) *WG_ST(o.reward, wrow, 1) = (cy + (-fdiv_count(rd[4], fM, yM)) * 0.1f) + neg_half_count(hits);
         if (o.done) {
             int done = steps >= kp.max_steps;
             if (!done && cy < kp.done_y) done = 1;
             if (!done && steps > 100) done = all;
-            o.done[wrow] = (uint8_t)done;
+            at_u32w(o.done, (uint32_t)wrow) = (uint8_t)done;
         }
         // the walker's mean position (np.mean: info's centroid, getstat's mid), once per walker: every mass lane of the
         // observation rows reads it from LDS instead of dividing again (-25 VALU per wave)
         const float mx = fdiv_count(rd[0], fM, yM), my = fdiv_count(rd[1], fM, yM), mz = fdiv_count(rd[2], fM, yM);
         s_mid[3 * lane] = mx; s_mid[3 * lane + 1] = my; s_mid[3 * lane + 2] = mz;
-        if (o.centroid) { o.centroid[3 * wrow] = mx; o.centroid[3 * wrow + 1] = my; o.centroid[3 * wrow + 2] = mz; }
-        if (o.energy) o.energy[wrow] = 0.5f * rd[5] + rd[6];
+        if (o.centroid) {
+            float *c = WG_ST(o.centroid, wrow, 3);
+            c[0] = mx; c[1] = my; c[2] = mz;
+        }
+        if (o.energy) *WG_ST(o.energy, wrow, 1) = 0.5f * rd[5] + rd[6];
     }
     wave_sync();
     STAMP(5);
@@ -2783,7 +2807,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
         typedef float fvd __attribute__((ext_vector_type(d), aligned(4)));
         if (is_mass) {
             const float *rd = kp.midform == 2 ? s_red + 8 * mw : s_mid + 3 * mw;   // G1 getstat: the SUM; else the mean
-            float *dst = o.obs + (size_t)s_row[mw] * stride + per * (lane - mlm);
+            float *dst = WG_ST(o.obs, (uint32_t)s_row[mw] * (uint32_t)stride + per * (lane - mlm), 1);
             const float pm[3] = {px, py, pz}, vm[3] = {vx, vy, vz}, am[3] = {ax, ay, az};
             fvd vp, vv, va;
 #pragma unroll
@@ -2799,18 +2823,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
         }
         if (lane < nw && nmid) {
             const int M = s_mo[lane + 1] - s_mo[lane];
-            float *row = o.obs + (size_t)wrow * stride + per * M;
+            float *row = WG_ST(o.obs, (uint32_t)wrow * (uint32_t)stride + per * M, 1);
             const float *rd = s_red + 8 * lane;
             for (int c = 0; c < 3; c++) row[c] = kp.midform == 2 ? rd[c] : kp.midform ? rd[c] / (float)M : 0.f;
         }
-        if (is_mus) o.obs[(size_t)s_row[uw] * stride + per * (s_mo[uw + 1] - s_mo[uw]) + nmid + ua] = x * kp.mk;
+        if (is_mus)
+            *WG_ST(o.obs, (uint32_t)s_row[uw] * (uint32_t)stride + per * (s_mo[uw + 1] - s_mo[uw]) + nmid + ua, 1) =
+                x * kp.mk;
         if (!o.obs_pad_clean) {
             // zeros from each row's own length to the stride; row w = i / stride
             const float inv = 1.f / (float)stride;
             for (int i = lane; i < nw * stride; i += 64) {
                 const int w = fdiv(i, stride, inv), c = i - w * stride;
                 const int len = per * (s_mo[w + 1] - s_mo[w]) + nmid + (s_uo[w + 1] - s_uo[w]);
-                if (c >= len) o.obs[(size_t)s_row[w] * stride + c] = 0.f;
+                if (c >= len) *WG_ST(o.obs, (uint32_t)s_row[w] * (uint32_t)stride + c, 1) = 0.f;
             }
         }
     }
@@ -3037,6 +3063,8 @@ bool u32_bytes(const wg_batch *b) {
     return (int64_t)b->N * b->M * 12 < lim && (int64_t)b->N * b->K * 16 < lim && (int64_t)b->N * b->A * 8 < lim &&
            (int64_t)b->N * (b->M + 1) * 2 < lim;
 }
+// and their observation rows as 32-bit byte offsets (WG_ST)
+bool obs_u32(const wg_batch *b, int obs_stride) { return (int64_t)b->N * std::max(obs_stride, 1) * 4 < (1ll << 32); }
 
 bool lean_geo(const wg_batch *b, int obs_stride, LeanGeo *out, int spring_mode = 0) {
     const int M = b->M;
@@ -3044,7 +3072,7 @@ bool lean_geo(const wg_batch *b, int obs_stride, LeanGeo *out, int spring_mode =
     if (spring_mode != 0) return false;          // the G2-compat element runs on the workgroup kernel
     // 32-bit element offsets inside the kernel, 32-bit byte offsets for its loads (at_u32)
     if ((int64_t)b->N * b->M * 3 >= (1ll << 31) || (int64_t)b->N * b->K * 4 >= (1ll << 31) ||
-        (int64_t)b->N * std::max(obs_stride, 1) >= (1ll << 31) || !u32_bytes(b))
+        !obs_u32(b, obs_stride) || !u32_bytes(b))
         return false;
     LeanGeo g{};
     g.wpw = 64 / M;
@@ -3144,12 +3172,11 @@ int wave_passes(int M, int K) {
 
 bool rag_geo(const wg_batch *b, int obs_stride, RagGeo *out) {
     const int ne = wave_passes(b->M, b->K);
-    if (b->ragged != 2 || ne == 0 || b->A > 64 || !u32_bytes(b)) return false;
+    if (b->ragged != 2 || ne == 0 || b->A > 64 || !u32_bytes(b) || !obs_u32(b, obs_stride)) return false;
     RagGeo g{};
     const int wpb = env_int("WG_LEAN_WAVES", 4);
     g.wpb = (wpb == 1 || wpb == 2) ? wpb : 4;
     const int ec = 64 * ne;                                      // spring slots of a tile
-    (void)obs_stride;                                            // observation rows go from registers to HBM
     // spring terms t (f64 x3), later the per-mass reduction terms | damping forces df, later the walker partials |
     // incidence words | muscle x | walker offsets and rows
     g.off_df = align16(std::max(ec * 24, 4 * 64 * 6));

@@ -36,7 +36,7 @@ geo = env.batch.launch_geometry()
 wpw = geo["walkers_per_block"] // max(1, geo["threads"] // 64)   # walkers per wave tile (lean kernel)
 W = env.batch.plan_blocks if env.batch.ragged else -(-N // wpw)     # waves (one tile each)
 st = np.zeros((W, 8), np.uint64)
-print("WG_LEAN_WAVES", os.environ.get("WG_LEAN_WAVES", "4"))
+print("WG_LEAN_WAVES", os.environ.get("WG_LEAN_WAVES", "auto"))
 L = _lib.load()
 L.wg_debug_stamps.argtypes = [C.c_void_p, C.c_int]
 assert L.wg_debug_stamps(st.ctypes.data_as(C.c_void_p), W) == 0

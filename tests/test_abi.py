@@ -210,13 +210,14 @@ def test_plan_waves_host(lib):
 
 
 def test_launch_geometry_small_batch_halves_tiles(lib):
-    """A uniform batch with fewer than 512 full wave tiles gets fewer walkers per wave (two tiles per CU)."""
+    """A uniform batch with fewer than 512 full wave tiles gets fewer walkers per wave (two tiles per CU), and a batch
+    of at most 1,024 tiles one wave per workgroup (the tiles spread over every CU)."""
     b = _lib.WgBatch(N=4096, M=4, K=5, A=2, ragged=0)
     for f in ("pos", "vel", "acc", "mass", "edges", "inc", "inc_off", "muscle_x", "steps"):
         setattr(b, f, 16)
     info = _lib.WgLaunchInfo()
     assert lib.wg_launch_geometry(C.byref(b), C.byref(info)) == 0
-    assert info.walkers_per_block == 4 * 8 and info.blocks == 128        # 8 Balance walkers per wave, 512 tiles
+    assert info.walkers_per_block == 8 and info.blocks == 512 and info.threads == 64   # 8 Balance walkers per wave
 
 
 def test_step_ranges_argument_errors(lib):

@@ -3085,8 +3085,11 @@ bool lean_geo(const wg_batch *b, int obs_stride, LeanGeo *out, int spring_mode =
     g.lgM = 0;
     while ((1 << g.lgM) < M) g.lgM++;
     if ((g.wpw * b->K + 63) / 64 > 8 || g.wpw * b->A > 64) return false;
-    const int wpb = env_int("WG_LEAN_WAVES", 4);
-    g.wpb = (wpb == 1 || wpb == 2) ? wpb : 4;
+    // waves per workgroup: 4 (one workgroup per four tiles) unless the batch has no more tiles than the chip has SIMDs,
+    // where one wave per workgroup spreads the latency-bound step over twice the CUs (4,096 Balance-v0 walkers: 5.45
+    // against 5.60 us, 65,536 canonical: 44.31 against 44.01; profiles/r04m_ab_*_wpb.json); WG_LEAN_WAVES overrides
+    const int wpb = env_int("WG_LEAN_WAVES", 0);
+    g.wpb = (wpb == 1 || wpb == 2 || wpb == 4) ? wpb : ((b->N + g.wpw - 1) / g.wpw <= 1024 ? 1 : 4);
     const int ew = g.wpw * b->K;                          // springs of a full wave tile
     g.pl = (ew + 3) & ~3;                                 // spring-term slots: 16-B aligned regions
     // t (f64 x3) | df (f32 x3) | incidence words | x (observation rows go from registers to HBM, no LDS tile)

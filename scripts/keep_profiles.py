@@ -23,8 +23,9 @@ for pre in sys.argv[1:]:
         name = os.path.basename(os.path.dirname(d))
         shutil.copy(d, os.path.join(P, name + "_kernel_stats.csv"))
         tr = os.path.join(os.path.dirname(d), "run_kernel_trace.csv")
+        # launches 200..399 of each grid: the bench's timed single-launch control (trace_kernels.py)
         subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "trace_kernels.py"), tr, "200",
-                        os.path.join(P, name + "_kernel_groups.json")], check=True, capture_output=True)
+                        os.path.join(P, name + "_kernel_groups.json"), "200"], check=True, capture_output=True)
         print("rocprof", name)
     for s in sorted(glob.glob(os.path.join(G, pre + "*_summary.json"))):
         name = os.path.basename(s)[:-len("_summary.json")]

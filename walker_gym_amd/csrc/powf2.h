@@ -11,8 +11,8 @@
  * unfused evaluation of the polynomials both match).
  *
  * pw_pow2(x) is the full evaluation.  pw_pow2_fast(x, &f) returns 1 and f = RN(x*x) when that provably equals it:
- * the double pre-rounding value of the algorithm lies within 1.69e-3 ulp of x^2 for every float (measured over all
- * of them), so when x^2 +- 2^-32 |x^2| (>= 1.95e-3 ulp) round to the same float, so does the algorithm's value.
+ * the double pre-rounding value of the algorithm lies within ~1.65e-3 ulp of x^2 for every float (measured over all
+ * of them), so when x^2 +- 1.75e-3 ulp round to the same float, so does the algorithm's value.
  */
 #ifndef WALKER_POWF2_H
 #define WALKER_POWF2_H
@@ -130,13 +130,31 @@ PW_FN float pw_pow2(float x) {
     return (float)(yy * s);
 }
 
-/* RN(x*x) when it provably equals pw_pow2(x) (returns 1), else 0 (call pw_pow2).  Finite x only. */
+/* RN(x*x) when it provably equals pw_pow2(x) (returns 1), else 0 (call pw_pow2).  Finite x only.
+ * The band: PW_FAST_C ulps of e's float binade (2^(E-24) for e = m 2^E, m in [0.5, 1)); e = 0 is exact.  1.75e-3 ulps
+ * sits just above the algorithm's largest deviation (the exhaustive sweep passes at 1.68e-3 and fails 1,274 inputs at
+ * 1.60e-3, profiles/r04_powf2_band.json) and sends 0.180 % of all floats to pw_pow2, against 0.293 % for the earlier
+ * relative band 2^-32 e (1.95e-3 to 3.9e-3 ulps across a binade; PW_FAST_C = 0 restores it). */
+#ifndef PW_FAST_C
+#define PW_FAST_C 1.75e-3
+#endif
 PW_FN int pw_pow2_fast(float x, float *out) {
     const double e = (double)x * (double)x;          /* exact: 48 significant bits */
-    const double d = e * 0x1p-32;
+    double d;
+    if (PW_FAST_C > 0.0) {
+#if defined(__HIPCC__) || defined(__HIP__)
+        d = __builtin_amdgcn_ldexp(PW_FAST_C, __builtin_amdgcn_frexp_exp(e) - 24);
+#else
+        int E;
+        (void)frexp(e, &E);
+        d = ldexp(PW_FAST_C, E - 24);
+#endif
+    } else {
+        d = e * 0x1p-32;
+    }
     const float lo = (float)(e - d), hi = (float)(e + d);
     *out = (float)e;
-    return lo == hi;
+    return lo == hi || e == 0.0;
 }
 
 #endif /* WALKER_POWF2_H */

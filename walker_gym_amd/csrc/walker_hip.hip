@@ -425,6 +425,78 @@ __device__ __forceinline__ float np_sq(float x) {
     if (__builtin_expect(!pw_pow2_fast(x, &f), 0) && WG_SQ_COLD) f = INL ? pw_pow2(x) : np_sq_cold(x);
     return f;
 }
+// The workgroup kernel's copy of glibc's powf tables in LDS (filled by its first 32 threads before its first barrier):
+// the cold path's two dependent table reads become LDS reads instead of global loads.  In the pair passes of the
+// performance_demo loop (gravity_vec's distance ** 2 for every partner) ~17 % of a wave's partner iterations take the
+// cold path: with the global tables it cost 21 % of the launch (188.5 against 149.6 us with RN(x*x) everywhere,
+// profiles/r04y_ab_perfdemo_sq.json).  pw_pow2's arithmetic, unchanged (powf2.h); checked on the GPU against pw_pow2
+// for every float32 bit pattern (scripts/check_pow2_lanes.hip).
+#ifndef WG_SQ_LDS
+#define WG_SQ_LDS 1
+#endif
+__shared__ double s_pw_log2[32];
+__shared__ unsigned long long s_pw_exp2[32];
+__device__ __forceinline__ void pw_tables_to_lds(int tid) {
+    if (tid < 32) { s_pw_log2[tid] = PW_LOG2_TAB[tid]; s_pw_exp2[tid] = PW_EXP2_TAB[tid]; }
+}
+#ifndef WG_SQ_LDS_INL
+#define WG_SQ_LDS_INL 1   // the LDS-table evaluation inline in the pair loop (0: a call; 186.9 against 183.5 us perfdemo)
+#endif
+template <bool INL>
+__device__ __forceinline__ float pw_pow2_lds_body(float x);
+__device__ __attribute__((noinline)) float pw_pow2_lds_call(float x) { return pw_pow2_lds_body<false>(x); }
+__device__ __forceinline__ float pw_pow2_lds(float x) {
+    return WG_SQ_LDS_INL ? pw_pow2_lds_body<true>(x) : pw_pow2_lds_call(x);
+}
+template <bool INL>
+__device__ __forceinline__ float pw_pow2_lds_body(float x) {
+    unsigned int ix = pw_asu32(x) & 0x7fffffffu;
+    if (ix == 0u || ix >= 0x7f800000u) return x * x;
+    if (ix < 0x00800000u) {
+        ix = pw_asu32(pw_asfloat(ix) * 0x1p23f) & 0x7fffffffu;
+        ix -= 23u << 23;
+    }
+    const unsigned int tmp = ix - 0x3f330000u;
+    const int i = (int)((tmp >> 19) & 15u);
+    const unsigned int top = tmp & 0xff800000u;
+    const int k = (int)top >> 23;
+    const double invc = s_pw_log2[2 * i], logc = s_pw_log2[2 * i + 1];
+    const double z = (double)pw_asfloat(ix - top);
+    const double r = PW_FMA(z, invc, -1.0);
+    const double y0 = logc + (double)k;
+    const double r2 = r * r;
+    double y = PW_FMA(0x1.27616c9496e0bp-2, r, -0x1.71969a075c67ap-2);
+    const double p = PW_FMA(0x1.ec70a6ca7baddp-2, r, -0x1.7154748bef6c8p-1);
+    const double r4 = r2 * r2;
+    double q = PW_FMA(0x1.71547652ab82bp+0, r, y0);
+    q = PW_FMA(p, r2, q);
+    y = PW_FMA(y, r4, q);
+    const double xd = 2.0 * y;
+    if (((pw_asu64(xd) >> 47) & 0xffffu) >= (pw_asu64(126.0) >> 47)) {
+        if (xd > 0x1.fffffffd1d571p+6) return pw_asfloat(0x7f800000u);
+        if (xd <= -150.0) return 0.0f;
+    }
+    const double shift = 0x1.8p+47;
+    double kd = xd + shift;
+    const unsigned long long ki = pw_asu64(kd);
+    kd -= shift;
+    const double rr = xd - kd;
+    const unsigned long long t = s_pw_exp2[ki & 31u] + (ki << 47);
+    const double sc = pw_asdouble(t);
+    const double zz = PW_FMA(0x1.c6af84b912394p-5, rr, 0x1.ebfce50fac4f3p-3);
+    const double rr2 = rr * rr;
+    double yy = PW_FMA(0x1.62e42ff0c52d6p-1, rr, 1.0);
+    yy = PW_FMA(zz, rr2, yy);
+    return (float)(yy * sc);
+}
+// np_sq with the cold path on the LDS tables (workgroup kernel only: the tables must have been filled)
+template <bool LDS_TAB>
+__device__ __forceinline__ float np_sq_t(float x) {
+    if (!(LDS_TAB && WG_SQ_LDS)) return np_sq(x);
+    float f;
+    if (__builtin_expect(!pw_pow2_fast(x, &f), 0) && WG_SQ_COLD) f = pw_pow2_lds(x);
+    return f;
+}
 
 // Global -> LDS copy of n 4-byte words (16-B vector loads when both ends allow it).
 template <typename T4, typename T1>
@@ -1158,11 +1230,12 @@ __device__ __forceinline__ float fdiv_rcp(float a, double y) { return (float)((d
 // reciprocals, the division by m from ym = RN64(1/m) (fdiv_exact).  ok = false when the squared distance leaves
 // [2^-96, 2^126) (sqrt_mid's range, which also keeps the distance clear of Config.r); the caller then takes
 // g2_gravity_cold for this partner.
+template <bool LDS_TAB = false>
 __device__ __forceinline__ void g2_gravity_fast(float cg, float d0, float d1, float d2, double ym, float &q0,
                                                 float &q1, float &q2, bool &ok) {
     const float sq = (float)(((double)(d0 * d0) + (double)(d1 * d1)) + (double)(d2 * d2));
     const float dist = sqrt_mid(sq);
-    const float dd = np_sq(dist);
+    const float dd = np_sq_t<LDS_TAB>(dist);
     const float f = fdiv_rcp(cg, rcp64_nr((double)dd));
     const double yd = rcp64_nr((double)dist);
     const float e0 = f * d0, e1 = f * d1, e2 = f * d2;
@@ -1173,11 +1246,12 @@ __device__ __forceinline__ void g2_gravity_fast(float cg, float d0, float d1, fl
     q1 = fdiv_exact(fdiv_rcp(e1, yd), ym);
     q2 = fdiv_exact(fdiv_rcp(e2, yd), ym);
 }
+template <bool LDS_TAB = false>
 __device__ __forceinline__ void g2_gravity_term(double cgd, float d0, float d1, float d2, float mf, double ym,
                                                 float &ax, float &ay, float &az) {
     float q0, q1, q2;
     bool ok = WG_FAST_PAIR;
-    if (WG_FAST_PAIR) g2_gravity_fast((float)cgd, d0, d1, d2, ym, q0, q1, q2, ok);
+    if (WG_FAST_PAIR) g2_gravity_fast<LDS_TAB>((float)cgd, d0, d1, d2, ym, q0, q1, q2, ok);
     if (__builtin_expect(!ok || !divisor_ok(mf), 0)) g2_gravity_cold(cgd, d0, d1, d2, mf, q0, q1, q2);
     ax = ax + q0;
     ay = ay + q1;
@@ -1294,8 +1368,8 @@ __device__ void pair_forces_lds(const wg_batch &b, const KParams &kp, const floa
             if (pj == q) continue;
             const float *o3 = spos + 3 * (lm + pj);
             const double mo = (double)sm[lm + pj];
-            g2_gravity_term(((-kp.pair_g) * (pj < q ? mo : md)) * (pj < q ? md : mo), o3[0] - p3[0], o3[1] - p3[1],
-                            o3[2] - p3[2], mf, ym, ax, ay, az);
+            g2_gravity_term<true>(((-kp.pair_g) * (pj < q ? mo : md)) * (pj < q ? md : mo), o3[0] - p3[0],
+                                  o3[1] - p3[1], o3[2] - p3[2], mf, ym, ax, ay, az);
         }
     }
     if (kp.pair_mode & 16)                   // Point.electrostatic (gym/engine.py:150-158) of every point
@@ -1426,6 +1500,7 @@ __global__ __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(wg_kernel_
         }
         s.x[u] = x;
     }
+    if (WG_SQ_LDS) pw_tables_to_lds(tid);   // (np_sq_t's cold path: the pair passes, the energy terms)
     __syncthreads();
 
     // registers of this lane's (first) mass after the physics: feed the SHFL reductions and obs
@@ -1519,7 +1594,7 @@ __global__ __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(wg_kernel_
             }
             // reduction terms of the new state: |v|, m*|v|^2, f32(m*g)*(y-ground)
             nv = np_norm3(vx, vy, vz);
-            ke = mf * np_sq(nv);   // p.m * norm(p.v) ** 2 (gym/optimized_env.py:242)
+            ke = mf * np_sq_t<true>(nv);   // p.m * norm(p.v) ** 2 (gym/optimized_env.py:242)
             pe = (float)(md * kp.g) * (py - kp.ground);
             if (!SHFL) { s.nrm[lp] = nv; s.ke[lp] = ke; s.pe[lp] = pe; }
         }
@@ -1535,7 +1610,7 @@ __global__ __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(wg_kernel_
                 ax = s.acc[3 * lp]; ay = s.acc[3 * lp + 1]; az = s.acc[3 * lp + 2];
             }
             nv = np_norm3(vx, vy, vz);
-            ke = mf * np_sq(nv);
+            ke = mf * np_sq_t<true>(nv);
             pe = (float)((double)mf * kp.g) * (py - kp.ground);
             if (!SHFL) { s.nrm[lp] = nv; s.ke[lp] = ke; s.pe[lp] = pe; }
         }
@@ -2035,7 +2110,7 @@ __device__ __forceinline__ double lane_gather_d(double v, int src_byte) {
 // Balance-4096 5.48 -> 5.37 us (the cold path, ~9 % of its waves, cost 0.28 us: RN(x*x) everywhere ran 5.20;
 // profiles/r04x_ab_balance_sq.json).
 #ifndef WG_SQ_REG
-#define WG_SQ_REG 1
+#define WG_SQ_REG 1   // 1: the lean NE = 1 tiles; 2 (A/B): every lean instance and the wave kernel
 #endif
 __device__ __forceinline__ float pw_pow2_lanes(float x, double tl, double te) {
     unsigned int ix = pw_asu32(x) & 0x7fffffffu;
@@ -2234,7 +2309,7 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
     const bool pin = L.pin != 0;
     // (WG_SQ_REG, NE = 1: glibc's powf tables in registers, lane l < 32 holding entry l of each)
     double sq_tl = 0.0, sq_te = 0.0;
-    if (WG_SQ_REG && NE == 1 && !RES) {   // (not the resident kernel: its carried state holds the registers)
+    if (WG_SQ_REG && (NE == 1 || WG_SQ_REG >= 2) && !RES) {   // (not the resident kernel: its carried state)
         sq_tl = PW_LOG2_TAB[lane & 31];
         sq_te = pw_asdouble(PW_EXP2_TAB[lane & 31]);
     }
@@ -2396,10 +2471,10 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
                   (WG_ENV_PRE && !RES) ? &et : nullptr);
         if (b.radius && store) b.radius[pl] = hit ? 3.0 : 1.0;   // p.r = 3 / p.r = 1 (gym/optimized_env.py:156,175)
         nv = np_norm3(vx, vy, vz);
-        if (!(WG_SQ_REG && NE == 1 && !RES)) ke = mf * np_sq<NE == 1>(nv);   // p.m * norm(p.v) ** 2 (gym/optimized_env.py:242)
+        if (!(WG_SQ_REG && (NE == 1 || WG_SQ_REG >= 2) && !RES)) ke = mf * np_sq<NE == 1>(nv);   // p.m * norm(p.v) ** 2 (gym/optimized_env.py:242)
         pe = (float)((double)mf * kp.g) * (py - kp.ground);
     }
-    if (WG_SQ_REG && NE == 1 && !RES) {   // every lane (table gathers); lanes past the masses square 0
+    if (WG_SQ_REG && (NE == 1 || WG_SQ_REG >= 2) && !RES) {   // every lane (table gathers); past the masses: 0
         const float sq = np_sq_wave(nv, sq_tl, sq_te);
         if (is_mass) ke = mf * sq;
     }
@@ -2816,8 +2891,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
         const float nv = nvm;
         s_tp[3 * lane] = px; s_tp[3 * lane + 1] = py; s_tp[3 * lane + 2] = pz;
         s_tn[lane] = nv;
-        s_tk[lane] = mf * np_sq(nv);   // p.m * norm(p.v) ** 2 (gym/optimized_env.py:242)
+        if (WG_SQ_REG < 2) s_tk[lane] = mf * np_sq(nv);   // p.m * norm(p.v) ** 2 (gym/optimized_env.py:242)
         s_te[lane] = (float)((double)mf * kp.g) * (py - kp.ground);
+    }
+    if (WG_SQ_REG >= 2) {   // (A/B) every lane: the register-table powf, lanes past the masses square 0
+        const double tl = PW_LOG2_TAB[lane & 31], te = pw_asdouble(PW_EXP2_TAB[lane & 31]);
+        const float sq = np_sq_wave(nvm, tl, te);
+        if (is_mass) s_tk[lane] = mf * sq;
     }
     wave_sync();
 
@@ -3100,7 +3180,10 @@ Geo ragged_geo(const wg_batch *b) {
 template <bool STEP, bool RAGGED, bool IN3D, int PWD, bool SHFL>
 int launch(const wg_batch *b, const KParams &kp, const float *action, int cols, int astride,
            const wg_outputs &o, const int32_t *plan, int blocks, const Geo &g, hipStream_t stream) {
-    if (g.lds > LDS_LIMIT) return fail(WG_ERANGE, "workgroup needs %d B of LDS (> 160 KiB)", g.lds);
+    // (+ the static 512 B of the powf tables, WG_SQ_LDS)
+    const int lds_static = WG_SQ_LDS ? (int)(sizeof(s_pw_log2) + sizeof(s_pw_exp2)) : 0;
+    if (g.lds + lds_static > LDS_LIMIT)
+        return fail(WG_ERANGE, "workgroup needs %d B of LDS (> 160 KiB)", g.lds + lds_static);
     hipLaunchKernelGGL((walker_step_kernel<STEP, RAGGED, IN3D, PWD, SHFL>), dim3(blocks), dim3(g.threads), g.lds, stream,
                        *b, kp, action, cols, astride, kout(o), plan, g);
     const hipError_t e = hipGetLastError();

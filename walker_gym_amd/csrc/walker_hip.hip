@@ -2110,7 +2110,7 @@ __device__ __forceinline__ double lane_gather_d(double v, int src_byte) {
 // Balance-4096 5.48 -> 5.37 us (the cold path, ~9 % of its waves, cost 0.28 us: RN(x*x) everywhere ran 5.20;
 // profiles/r04x_ab_balance_sq.json).
 #ifndef WG_SQ_REG
-#define WG_SQ_REG 1   // 1: the lean NE = 1 tiles; 2 (A/B): every lean instance and the wave kernel
+#define WG_SQ_REG 1
 #endif
 __device__ __forceinline__ float pw_pow2_lanes(float x, double tl, double te) {
     unsigned int ix = pw_asu32(x) & 0x7fffffffu;
@@ -2309,7 +2309,7 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
     const bool pin = L.pin != 0;
     // (WG_SQ_REG, NE = 1: glibc's powf tables in registers, lane l < 32 holding entry l of each)
     double sq_tl = 0.0, sq_te = 0.0;
-    if (WG_SQ_REG && (NE == 1 || WG_SQ_REG >= 2) && !RES) {   // (not the resident kernel: its carried state)
+    if (WG_SQ_REG && NE == 1 && !RES) {   // (not the resident kernel: its carried state holds the registers)
         sq_tl = PW_LOG2_TAB[lane & 31];
         sq_te = pw_asdouble(PW_EXP2_TAB[lane & 31]);
     }
@@ -2471,10 +2471,10 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
                   (WG_ENV_PRE && !RES) ? &et : nullptr);
         if (b.radius && store) b.radius[pl] = hit ? 3.0 : 1.0;   // p.r = 3 / p.r = 1 (gym/optimized_env.py:156,175)
         nv = np_norm3(vx, vy, vz);
-        if (!(WG_SQ_REG && (NE == 1 || WG_SQ_REG >= 2) && !RES)) ke = mf * np_sq<NE == 1>(nv);   // p.m * norm(p.v) ** 2 (gym/optimized_env.py:242)
+        if (!(WG_SQ_REG && NE == 1 && !RES)) ke = mf * np_sq<NE == 1>(nv);   // p.m * norm(p.v) ** 2 (gym/optimized_env.py:242)
         pe = (float)((double)mf * kp.g) * (py - kp.ground);
     }
-    if (WG_SQ_REG && (NE == 1 || WG_SQ_REG >= 2) && !RES) {   // every lane (table gathers); past the masses: 0
+    if (WG_SQ_REG && NE == 1 && !RES) {   // every lane (table gathers); lanes past the masses square 0
         const float sq = np_sq_wave(nv, sq_tl, sq_te);
         if (is_mass) ke = mf * sq;
     }
@@ -2891,13 +2891,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
         const float nv = nvm;
         s_tp[3 * lane] = px; s_tp[3 * lane + 1] = py; s_tp[3 * lane + 2] = pz;
         s_tn[lane] = nv;
-        if (WG_SQ_REG < 2) s_tk[lane] = mf * np_sq(nv);   // p.m * norm(p.v) ** 2 (gym/optimized_env.py:242)
+        s_tk[lane] = mf * np_sq(nv);   // p.m * norm(p.v) ** 2 (gym/optimized_env.py:242)
         s_te[lane] = (float)((double)mf * kp.g) * (py - kp.ground);
-    }
-    if (WG_SQ_REG >= 2) {   // (A/B) every lane: the register-table powf, lanes past the masses square 0
-        const double tl = PW_LOG2_TAB[lane & 31], te = pw_asdouble(PW_EXP2_TAB[lane & 31]);
-        const float sq = np_sq_wave(nvm, tl, te);
-        if (is_mass) s_tk[lane] = mf * sq;
     }
     wave_sync();
 

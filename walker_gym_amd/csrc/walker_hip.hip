@@ -490,11 +490,18 @@ __device__ __forceinline__ float pw_pow2_lds_body(float x) {
     return (float)(yy * sc);
 }
 // np_sq with the cold path on the LDS tables (workgroup kernel only: the tables must have been filled)
+#if WG_SQ_COLD == 2
+__device__ int g_sq_never;   // (timing builds: a cold path the compiler must keep but the run never takes)
+#endif
 template <bool LDS_TAB>
 __device__ __forceinline__ float np_sq_t(float x) {
     if (!(LDS_TAB && WG_SQ_LDS)) return np_sq(x);
     float f;
+#if WG_SQ_COLD == 2
+    if (__builtin_expect(!pw_pow2_fast(x, &f), 0) && __builtin_nontemporal_load(&g_sq_never)) f = pw_pow2_lds(x);
+#else
     if (__builtin_expect(!pw_pow2_fast(x, &f), 0) && WG_SQ_COLD) f = pw_pow2_lds(x);
+#endif
     return f;
 }
 

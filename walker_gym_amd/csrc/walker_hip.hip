@@ -1086,8 +1086,11 @@ __device__ inline WalkerSums walker_sums(float px, float py, float pz, float nv,
     WalkerSums r;
     if (WG_SUMS7 && M == 4) {
         // a walker is one DPP quad: every lane adds the quad's four values in order (M < 8: pairwise == sequential)
-        float a = 0.f + quad_bcast<0>(px), b = 0.f + quad_bcast<0>(py), c = 0.f + quad_bcast<0>(pz);
-        float d = 0.f + quad_bcast<0>(nv), e = 0.f + quad_bcast<0>(ke), f = 0.f + quad_bcast<0>(pe);
+        // (x_0 + 0 with the zero in a register: one v_add_f32_dpp each, no separate DPP move; x + 0 == 0 + x)
+        float z = 0.f;
+        asm volatile("" : "+v"(z));
+        float a = quad_bcast<0>(px) + z, b = quad_bcast<0>(py) + z, c = quad_bcast<0>(pz) + z;
+        float d = quad_bcast<0>(nv) + z, e = quad_bcast<0>(ke) + z, f = quad_bcast<0>(pe) + z;
         WG_OPAQUE7(a, b, c, d, e, f, py);
         a = a + quad_bcast<1>(px); b = b + quad_bcast<1>(py); c = c + quad_bcast<1>(pz);
         d = d + quad_bcast<1>(nv); e = e + quad_bcast<1>(ke); f = f + quad_bcast<1>(pe);
@@ -1095,8 +1098,14 @@ __device__ inline WalkerSums walker_sums(float px, float py, float pz, float nv,
         a = a + quad_bcast<2>(px); b = b + quad_bcast<2>(py); c = c + quad_bcast<2>(pz);
         d = d + quad_bcast<2>(nv); e = e + quad_bcast<2>(ke); f = f + quad_bcast<2>(pe);
         WG_OPAQUE7(a, b, c, d, e, f, py);
-        a = a + quad_bcast<3>(px); b = b + quad_bcast<3>(py); c = c + quad_bcast<3>(pz);
-        d = d + quad_bcast<3>(nv); e = e + quad_bcast<3>(ke); f = f + quad_bcast<3>(pe);
+        // (one add at a time behind an empty asm: otherwise SLP pairs the last step's adds into v_pk_add_f32, which takes
+        // no DPP operand, and each pair costs two DPP moves more)
+        a = a + quad_bcast<3>(px); asm volatile("" : "+v"(a));
+        b = b + quad_bcast<3>(py); asm volatile("" : "+v"(b));
+        c = c + quad_bcast<3>(pz); asm volatile("" : "+v"(c));
+        d = d + quad_bcast<3>(nv); asm volatile("" : "+v"(d));
+        e = e + quad_bcast<3>(ke); asm volatile("" : "+v"(e));
+        f = f + quad_bcast<3>(pe);
         r.sx = a; r.sy = b; r.sz = c; r.ysum = b; r.vsum = d; r.ksum = e; r.psum = f;
         return r;
     }

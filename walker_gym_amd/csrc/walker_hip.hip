@@ -1119,7 +1119,11 @@ __device__ inline WalkerSums walker_sums(float px, float py, float pz, float nv,
         WG_OPAQUE7(a, b, c, y, v, k, e);
         y = y + dpp_f<0x4E>(y); v = v + dpp_f<0x4E>(v); k = k + dpp_f<0x4E>(k); e = e + dpp_f<0x4E>(e);
         WG_OPAQUE7(a, b, c, y, v, k, e);
-        y = y + dpp_f<0x141>(y); v = v + dpp_f<0x141>(v); k = k + dpp_f<0x141>(k); e = e + dpp_f<0x141>(e);
+        // (the last step one add at a time: SLP would pair them into v_pk_add_f32, two DPP moves per pair)
+        y = y + dpp_f<0x141>(y); asm volatile("" : "+v"(y));
+        v = v + dpp_f<0x141>(v); asm volatile("" : "+v"(v));
+        k = k + dpp_f<0x141>(k); asm volatile("" : "+v"(k));
+        e = e + dpp_f<0x141>(e); asm volatile("" : "+v"(e));
 #pragma unroll
         for (int t = 1; t < 16; t++) {
             a = dpp_f<0x111>(a) + px; b = dpp_f<0x111>(b) + py; c = dpp_f<0x111>(c) + pz;

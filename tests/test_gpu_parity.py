@@ -475,8 +475,9 @@ def test_resident_rollout_bit_identical(case):
         assert np.array_equal(a.numpy(), b.numpy(), equal_nan=a.dtype.is_floating_point), (case, k)
 
 
-def test_run_lanes_bit_identical():
-    """run() with the walkers split over 2 / 3 streams (lanes) gives the same bits as one stream."""
+def test_run_lanes_bit_identical(monkeypatch):
+    """run() with the walkers split over 2 / 3 streams (lanes) gives the same bits as one stream, with the ranges
+    issued step by step (wg_run_ranges, the default) and range by range (WG_RANGE_ISSUE=seq)."""
     import torch
     from walker_gym_amd.batched_env import BatchedPhysicsEnv
     from walker_gym_amd.synthetic import canonical_walkers
@@ -486,7 +487,8 @@ def test_run_lanes_bit_identical():
             * 2 - 1).contiguous()
     sd0 = env.batch.state_dict()
     ref = None
-    for lanes in (1, 2, 3):
+    for lanes, issue in ((1, "inter"), (2, "inter"), (3, "inter"), (2, "seq")):
+        monkeypatch.setenv("WG_RANGE_ISSUE", issue)
         env.batch.load_state_dict(sd0)
         env.run(acts, 40, lanes=lanes)
         torch.cuda.synchronize()
@@ -504,12 +506,14 @@ def test_run_lanes_bit_identical():
                      device="cuda:0") * 2 - 1).contiguous()
     rsd = rg.batch.state_dict()
     rres = []
-    for lanes in (1, 2):
+    for lanes, issue in ((1, "inter"), (2, "inter"), (2, "seq")):
+        monkeypatch.setenv("WG_RANGE_ISSUE", issue)
         rg.batch.load_state_dict(rsd)
         rg.run(ra, 20, lanes=lanes)
         torch.cuda.synchronize()
         rres.append([t.clone() for t in rg.batch.state_dict().values()] + [rg.obs.clone(), rg.reward.clone()])
-    assert all(torch.equal(a, b) for a, b in zip(*rres))
+    assert all(torch.equal(a, b) for a, b in zip(rres[0], rres[1])) and all(torch.equal(a, b) for a, b in zip(rres[0], rres[2]))
+    monkeypatch.setenv("WG_RANGE_ISSUE", "inter")
     # rollout(): per-step outputs of every range land in the right rows
     outs = []
     for lanes in (1, 2):

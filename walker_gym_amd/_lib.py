@@ -13,7 +13,7 @@ import threading
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libwalker_hip.so"
 LIB_PATH = os.path.join(HERE, LIB_NAME)
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 WG_EINVAL, WG_ERANGE, WG_EHIP = -1, -2, -3
 
@@ -59,7 +59,7 @@ class WgLaunchInfo(C.Structure):
                 ("lds_bytes", C.c_int32)]
 
 
-EXPORTS = ("wg_abi_version", "wg_last_error", "wg_step", "wg_step_ranges", "wg_rollout", "wg_observe", "wg_reset", "wg_reset_noise",
+EXPORTS = ("wg_abi_version", "wg_last_error", "wg_step", "wg_step_ranges", "wg_run_ranges", "wg_rollout", "wg_observe", "wg_reset", "wg_reset_noise",
            "wg_plan_ragged", "wg_plan_waves", "wg_wave_edge_passes", "wg_plan_errors", "wg_launch_geometry", "wg_launch_floor")
 
 _lib = None
@@ -89,6 +89,8 @@ def load(path: str | None = None):
         L.wg_rollout.argtypes = L.wg_step.argtypes
         L.wg_step_ranges.argtypes = [C.POINTER(WgRange), C.c_int32, C.POINTER(WgParams), _vp, C.c_int32, C.c_int32,
                                      C.POINTER(_vp)]
+        L.wg_run_ranges.argtypes = [C.POINTER(WgRange), C.c_int32, C.POINTER(WgParams), _vp, C.c_int32, C.c_int32,
+                                    C.c_int64, C.c_int32, C.POINTER(_vp)]
         L.wg_observe.argtypes = [C.POINTER(WgBatch), C.POINTER(WgParams), C.POINTER(WgOutputs), _vp, C.c_int32, _vp]
         L.wg_reset.argtypes = [C.POINTER(WgBatch), C.POINTER(WgParams), _vp, _vp, _vp]
         L.wg_reset_noise.argtypes = [C.POINTER(WgBatch), _vp, _vp]
@@ -98,7 +100,7 @@ def load(path: str | None = None):
         L.wg_plan_errors.argtypes = [C.c_int32]
         L.wg_launch_geometry.argtypes = [C.POINTER(WgBatch), C.POINTER(WgLaunchInfo)]
         L.wg_launch_floor.argtypes = [C.c_int32, C.c_int32, C.c_int32, _vp, _vp, C.c_int32, _vp]
-        for f in ("wg_step", "wg_step_ranges", "wg_rollout", "wg_observe", "wg_reset", "wg_reset_noise", "wg_plan_ragged", "wg_plan_waves",
+        for f in ("wg_step", "wg_step_ranges", "wg_run_ranges", "wg_rollout", "wg_observe", "wg_reset", "wg_reset_noise", "wg_plan_ragged", "wg_plan_waves",
                   "wg_wave_edge_passes", "wg_plan_errors", "wg_launch_geometry", "wg_launch_floor"):
             getattr(L, f).restype = C.c_int
         v = L.wg_abi_version()

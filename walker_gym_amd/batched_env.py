@@ -479,8 +479,6 @@ class BatchedPhysicsEnv:
         T, n, cols = actions.shape
         cur = torch.cuda.current_stream(self.device)
         self.reserve_streams(lanes)
-        start = torch.cuda.Event()
-        start.record(cur)
         L = _lib.load()
         ragged = self.batch.ragged
         if ragged:   # ranges of plan blocks: the same batch, a slice of its block -> walker plan
@@ -488,6 +486,32 @@ class BatchedPhysicsEnv:
             bounds = [nb * i // lanes for i in range(lanes)] + [nb]
         else:
             bounds = [0] + [((self.N * i // lanes) + 63) // 64 * 64 for i in range(1, lanes)] + [self.N]
+        capturing = torch.cuda.is_current_stream_capturing()
+        if entry == "wg_step" and not capturing and os.environ.get("WG_RANGE_ISSUE", "seq") == "inter":
+            # one wg_run_ranges call: step s of every range issued before step s + 1 of any (default WG_RANGE_ISSUE=seq:
+            # range by range, one wg_step call each)
+            rng, keep = (_lib.WgRange * lanes)(), []
+            for i in range(lanes):
+                w0, w1 = bounds[i], bounds[i + 1]
+                if ragged:
+                    o, rng[i].batch, rng[i].action_offset = outputs(0, self.N), C.pointer(self.batch.struct), 0
+                    rng[i].plan, rng[i].plan_blocks = self.batch.plan.data_ptr() + 4 * w0, w1 - w0
+                else:
+                    sub = self.batch.sub_struct(w0, w1)
+                    keep.append(sub)
+                    o, rng[i].batch, rng[i].action_offset = outputs(w0, w1), C.pointer(sub), w0 * cols
+                    rng[i].plan, rng[i].plan_blocks = None, 0
+                keep.append(o)
+                rng[i].outputs = C.pointer(o)
+                rng[i].stream = (cur if i == 0 else self._side[i - 1]).cuda_stream
+            _lib.check(L.wg_run_ranges(rng, lanes, C.byref(self._pstruct), C.c_void_p(actions.data_ptr()), cols, cols,
+                                       0 if T == 1 else self.N * cols, n_steps, self._range_events(lanes)),
+                       "wg_run_ranges")
+            for st in self._side[:lanes - 1]:
+                actions.record_stream(st)   # the allocator must not recycle it before the side streams are done
+            return
+        start = torch.cuda.Event()
+        start.record(cur)
         done = []
         for i in range(lanes):
             w0, w1 = bounds[i], bounds[i + 1]
@@ -504,13 +528,24 @@ class BatchedPhysicsEnv:
                                          0 if T == 1 else self.N * cols, C.byref(o), n_steps, plan, nblk,
                                          C.c_void_p(st.cuda_stream)), entry)
             if i:
-                if not torch.cuda.is_current_stream_capturing():
+                if not capturing:
                     actions.record_stream(st)   # the allocator must not recycle it before the side stream is done
                 ev = torch.cuda.Event()
                 ev.record(st)
                 done.append(ev)
         for ev in done:
             cur.wait_event(ev)
+
+    def _range_events(self, lanes: int):
+        """wg_run_ranges' fork / join events (hipEvent handles of torch events, created once per env and reused: each
+        call records and waits on them stream-ordered)."""
+        ev = getattr(self, "_run_events", None)
+        if ev is None or len(ev[0]) < lanes:
+            objs = [torch.cuda.Event() for _ in range(lanes)]
+            for e in objs:
+                e.record()                       # materialise the hipEvent handle
+            ev = self._run_events = (objs, (C.c_void_p * lanes)(*[e.cuda_event for e in objs]))
+        return ev[1]
 
     def policy_loop(self, policy, n_steps: int, lanes: Optional[int] = None, graph: bool = False) -> None:
         """A closed loop with a per-walker policy, the walker ranges pipelined: at every step, each range computes its

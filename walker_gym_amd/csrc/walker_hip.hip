@@ -3414,7 +3414,7 @@ int dispatch(const wg_batch *b, const KParams &kp, bool in3d, const float *a, in
 
 int run(const wg_batch *b, const wg_params *p, const float *action, int32_t cols, int32_t astride,
         int64_t astep, const wg_outputs *o, int32_t n_steps, const int32_t *plan, int32_t plan_blocks,
-        hipStream_t stream, bool step, bool resident = false, bool check_only = false) {
+        hipStream_t stream, bool step, bool resident = false, bool check_only = false, int s_first = 0) {
     int rc = validate(b);
     if (rc) return rc;
     if (!p) return fail(WG_EINVAL, "null params");
@@ -3459,7 +3459,7 @@ int run(const wg_batch *b, const wg_params *p, const float *action, int32_t cols
     if (resident && use_lean && p->pair_mode == 0 && !extras)   // one launch for every step, state in registers
         return launch_lean_rollout(b, kp, p->in3d != 0, action, cols, astride, action ? astep : 0, out, n_steps, lg,
                                    stream);
-    for (int s = 0; s < n_steps; s++) {
+    for (int s = s_first; s < s_first + n_steps; s++) {   // (s_first: wg_run_ranges issues one step per call)
         wg_outputs os = out;
         if (os.obs) os.obs += s * os.obs_step;
         if (os.reward) os.reward += s * os.out_step;
@@ -3507,28 +3507,40 @@ int wg_rollout(const wg_batch *b, const wg_params *p, const float *action, int32
                true);
 }
 
-int wg_step_ranges(const wg_range *ranges, int32_t n, const wg_params *p, const float *action, int32_t action_cols,
-                   int32_t action_stride, hipEvent_t *events) {
-    if (!ranges || n < 1 || (n > 1 && !events)) return fail(WG_EINVAL, "wg_step_ranges: bad ranges / events");
+int wg_run_ranges(const wg_range *ranges, int32_t n, const wg_params *p, const float *action, int32_t action_cols,
+                  int32_t action_stride, int64_t action_step, int32_t n_steps, hipEvent_t *events) {
+    if (!ranges || n < 1 || (n > 1 && !events)) return fail(WG_EINVAL, "wg_run_ranges: bad ranges / events");
     // every range checked before the first launch: a bad range fails the call with no walker stepped
     for (int i = 0; i < n; i++) {
         const wg_range &r = ranges[i];
-        const int rc = run(r.batch, p, action ? action + r.action_offset : nullptr, action_cols, action_stride, 0,
-                           r.outputs, 1, r.plan, r.plan_blocks, r.stream, true, false, true);
+        const int rc = run(r.batch, p, action ? action + r.action_offset : nullptr, action_cols, action_stride,
+                           action_step, r.outputs, n_steps, r.plan, r.plan_blocks, r.stream, true, false, true);
         if (rc) return rc;
     }
+    if (n_steps <= 0) return 0;
     hipStream_t s0 = ranges[0].stream;
     if (n > 1 && hipEventRecord(events[0], s0) != hipSuccess) return fail(WG_EHIP, "fork event record failed");
-    for (int i = 0; i < n; i++) {
-        const wg_range &r = ranges[i];
-        if (i && hipStreamWaitEvent(r.stream, events[0], 0) != hipSuccess) return fail(WG_EHIP, "fork wait failed");
-        const int rc = run(r.batch, p, action ? action + r.action_offset : nullptr, action_cols, action_stride, 0,
-                           r.outputs, 1, r.plan, r.plan_blocks, r.stream, true);
-        if (rc) return rc;
-        if (i && (hipEventRecord(events[i], r.stream) != hipSuccess || hipStreamWaitEvent(s0, events[i], 0) != hipSuccess))
+    for (int i = 1; i < n; i++)
+        if (hipStreamWaitEvent(ranges[i].stream, events[0], 0) != hipSuccess) return fail(WG_EHIP, "fork wait failed");
+    // step s of every range is issued before step s + 1 of any: the ranges start together and stay side by side in
+    // the hardware queues (range by range, the second range would start only after the host had issued all of the
+    // first range's launches)
+    for (int s = 0; s < n_steps; s++)
+        for (int i = 0; i < n; i++) {
+            const wg_range &r = ranges[i];
+            const int rc = run(r.batch, p, action ? action + r.action_offset : nullptr, action_cols, action_stride,
+                               action_step, r.outputs, 1, r.plan, r.plan_blocks, r.stream, true, false, false, s);
+            if (rc) return rc;
+        }
+    for (int i = 1; i < n; i++)
+        if (hipEventRecord(events[i], ranges[i].stream) != hipSuccess || hipStreamWaitEvent(s0, events[i], 0) != hipSuccess)
             return fail(WG_EHIP, "join event failed");
-    }
     return 0;
+}
+
+int wg_step_ranges(const wg_range *ranges, int32_t n, const wg_params *p, const float *action, int32_t action_cols,
+                   int32_t action_stride, hipEvent_t *events) {
+    return wg_run_ranges(ranges, n, p, action, action_cols, action_stride, 0, 1, events);
 }
 
 int wg_observe(const wg_batch *b, const wg_params *p, const wg_outputs *o, const int32_t *plan,

@@ -211,6 +211,19 @@ class BatchedPhysicsEnv:
                               obs_pad_clean=int(pad_clean), steps=p(steps), nonfinite=p(nonfinite),
                               momentum=p(momentum))
 
+    @staticmethod
+    def _range_outputs(o, w0: int):
+        """The WgOutputs of a uniform walker range starting at walker w0: o's pointers advanced by w0 rows (every output
+        is walker-major: obs rows of obs_stride floats, f32 reward / energy, 1-byte done / nonfinite, int32 steps,
+        3 x f32 centroid / momentum).  Pointer arithmetic instead of tensor slices: no per-call tensor views."""
+        def adv(ptr, nbytes):
+            return None if not ptr else C.c_void_p(ptr + nbytes)
+        return _lib.WgOutputs(obs=adv(o.obs, 4 * w0 * o.obs_stride), obs_stride=o.obs_stride,
+                              reward=adv(o.reward, 4 * w0), done=adv(o.done, w0), centroid=adv(o.centroid, 12 * w0),
+                              energy=adv(o.energy, 4 * w0), obs_step=o.obs_step, out_step=o.out_step,
+                              obs_pad_clean=o.obs_pad_clean, steps=adv(o.steps, 4 * w0),
+                              nonfinite=adv(o.nonfinite, w0), momentum=adv(o.momentum, 12 * w0))
+
     def _extra_out(self, w0: int = 0, w1: Optional[int] = None) -> dict:
         """The opt-in info outputs of walkers [w0, w1) (or none)."""
         if not self._extras:
@@ -365,13 +378,11 @@ class BatchedPhysicsEnv:
         # (only where the resident kernel actually runs: otherwise the default walker ranges keep their overlap)
         lanes = self._lanes(1 if (resident and lanes is None and self.resident_ok()) else lanes) if T > 0 else 1
         entry = "wg_rollout" if resident else "wg_step"
-        if lanes > 1:
-            self._run_lanes(actions, T, lambda w0, w1: self._outputs(
-                obs_out[0, w0:w1], reward_out[0, w0:w1], done_out[0, w0:w1], None, None,
-                obs_step=self.N * self.obs_dim, out_step=self.N, pad_clean=clean), lanes, entry=entry)
-            return obs_out, reward_out, done_out
         o = self._outputs(obs_out, reward_out, done_out, None, None, obs_step=self.N * self.obs_dim,
                           out_step=self.N, pad_clean=clean)
+        if lanes > 1:
+            self._run_lanes(actions, T, o, lanes, entry=entry)
+            return obs_out, reward_out, done_out
         _lib.check(getattr(_lib.load(), entry)(
             C.byref(self.batch.struct), C.byref(self._pstruct), C.c_void_p(actions.data_ptr()), cols, cols,
             self.N * cols, C.byref(o), T,
@@ -417,16 +428,12 @@ class BatchedPhysicsEnv:
         if not info:
             cen = en = None
         # the opt-in info extras follow the last step only when the outputs are overwritten each step (no record)
-        ex = (lambda w0, w1: self._extra_out(w0, w1)) if (info and record is None) else (lambda w0, w1: {})
+        o = self._outputs(self.obs, rew, done, cen, en, pad_clean=True, steps=so, out_step=out_step,
+                          **(self._extra_out() if (info and record is None) else {}))
         if lanes > 1:
-            self._run_lanes(actions, int(n_steps), lambda w0, w1: self._outputs(
-                self.obs[w0:w1], rew[w0:w1], done[w0:w1], None if cen is None else cen[w0:w1],
-                None if en is None else en[w0:w1], pad_clean=True, steps=None if so is None else so[w0:w1],
-                out_step=out_step, **ex(w0, w1)), lanes, entry=entry)
+            self._run_lanes(actions, int(n_steps), o, lanes, entry=entry)
             self._steps_at = self.batch.version if so is not None else -1
             return
-        o = self._outputs(self.obs, rew, done, cen, en, pad_clean=True, steps=so, out_step=out_step,
-                          **ex(0, self.N))
         _lib.check(getattr(_lib.load(), entry)(
             C.byref(self.batch.struct), C.byref(self._pstruct), C.c_void_p(actions.data_ptr()), cols, cols,
             0 if T == 1 else self.N * cols, C.byref(o), int(n_steps),
@@ -470,12 +477,21 @@ class BatchedPhysicsEnv:
         while len(self._side) < lanes - 1:
             self._side.append(torch.cuda.Stream(device=self.device))
 
-    def _run_lanes(self, actions, n_steps: int, outputs, lanes: int, entry: str = "wg_step"):
+    def _range_batches(self, lanes: int, bounds) -> list:
+        """The per-range WgBatch views of a uniform batch, cached per batch struct (rebuilt whenever the batch's
+        arrays are: enable_radius) and walker ranges; the cache holds the struct, so its identity is not reused."""
+        key, st = (self._generation, tuple(bounds)), self.batch.struct
+        cached = getattr(self, "_range_cache", None)
+        if cached is None or cached[0] != key or cached[1] is not st:
+            cached = self._range_cache = (key, st, [self.batch.sub_struct(bounds[i], bounds[i + 1]) for i in range(lanes)])
+        return cached[2]
+
+    def _run_lanes(self, actions, n_steps: int, o_full, lanes: int, entry: str = "wg_step"):
         """n_steps with the walkers split into `lanes` contiguous ranges, each stepped by its own stream: the
         ranges are independent, so one range's step t + 1 fills the GPU while another's step t drains (the
         launch tail).  Every walker still takes every step, one launch per step per range; the calling
-        stream waits for all ranges before returning (stream-ordered, no host sync).  outputs(w0, w1) gives
-        the WgOutputs of walkers [w0, w1)."""
+        stream waits for all ranges before returning (stream-ordered, no host sync).  o_full: the whole batch's
+        WgOutputs (a uniform range's are its pointers advanced to the range's first walker)."""
         T, n, cols = actions.shape
         cur = torch.cuda.current_stream(self.device)
         self.reserve_streams(lanes)
@@ -487,19 +503,19 @@ class BatchedPhysicsEnv:
         else:
             bounds = [0] + [((self.N * i // lanes) + 63) // 64 * 64 for i in range(1, lanes)] + [self.N]
         capturing = torch.cuda.is_current_stream_capturing()
-        if entry == "wg_step" and not capturing and os.environ.get("WG_RANGE_ISSUE", "seq") == "inter":
-            # one wg_run_ranges call: step s of every range issued before step s + 1 of any (default WG_RANGE_ISSUE=seq:
-            # range by range, one wg_step call each)
+        if entry == "wg_step" and not capturing and os.environ.get("WG_RANGE_ISSUE", "inter") != "seq":
+            # one wg_run_ranges call: step s of every range issued before step s + 1 of any (WG_RANGE_ISSUE=seq:
+            # range by range, one wg_step call each: the last range starts only after the host has issued every
+            # launch of the ranges before it; scripts/issue_ab.sh)
             rng, keep = (_lib.WgRange * lanes)(), []
+            subs = None if ragged else self._range_batches(lanes, bounds)
             for i in range(lanes):
                 w0, w1 = bounds[i], bounds[i + 1]
                 if ragged:
-                    o, rng[i].batch, rng[i].action_offset = outputs(0, self.N), C.pointer(self.batch.struct), 0
+                    o, rng[i].batch, rng[i].action_offset = o_full, C.pointer(self.batch.struct), 0
                     rng[i].plan, rng[i].plan_blocks = self.batch.plan.data_ptr() + 4 * w0, w1 - w0
                 else:
-                    sub = self.batch.sub_struct(w0, w1)
-                    keep.append(sub)
-                    o, rng[i].batch, rng[i].action_offset = outputs(w0, w1), C.pointer(sub), w0 * cols
+                    o, rng[i].batch, rng[i].action_offset = self._range_outputs(o_full, w0), C.pointer(subs[i]), w0 * cols
                     rng[i].plan, rng[i].plan_blocks = None, 0
                 keep.append(o)
                 rng[i].outputs = C.pointer(o)
@@ -519,10 +535,10 @@ class BatchedPhysicsEnv:
             if i:
                 st.wait_event(start)
             if ragged:
-                sub, o, act = self.batch.struct, outputs(0, self.N), C.c_void_p(actions.data_ptr())
+                sub, o, act = self.batch.struct, o_full, C.c_void_p(actions.data_ptr())
                 plan, nblk = C.c_void_p(self.batch.plan.data_ptr() + 4 * w0), w1 - w0
             else:
-                sub, o = self.batch.sub_struct(w0, w1), outputs(w0, w1)
+                sub, o = self.batch.sub_struct(w0, w1), self._range_outputs(o_full, w0)
                 act, plan, nblk = C.c_void_p(actions.data_ptr() + 4 * w0 * cols), None, 0
             _lib.check(getattr(L, entry)(C.byref(sub), C.byref(self._pstruct), act, cols, cols,
                                          0 if T == 1 else self.N * cols, C.byref(o), n_steps, plan, nblk,

@@ -3480,6 +3480,14 @@ int run(const wg_batch *b, const wg_params *p, const float *action, int32_t cols
     return 0;
 }
 
+// wg_run_ranges' phase skew (WG_RANGE_SKEW_US): one wave that waits `ticks` of the 100 MHz constant clock before a
+// range's first step, so that range starts that much after the range before it and the ranges' launch drains fall
+// apart from the first step (the wait ends on every path: the clock only advances)
+__global__ __launch_bounds__(64) void range_skew_kernel(long long ticks) {
+    const long long t0 = wall_clock64();
+    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(4);
+}
+
 // the launch floor beside a small step (bench.py): an empty launch, and one coalesced load + store per thread
 __global__ __launch_bounds__(1024) void floor_empty_kernel(float *) {}
 __global__ __launch_bounds__(1024) void floor_load_store_kernel(const float *__restrict__ in, float *__restrict__ out) {
@@ -3524,14 +3532,27 @@ int wg_run_ranges(const wg_range *ranges, int32_t n, const wg_params *p, const f
         if (hipStreamWaitEvent(ranges[i].stream, events[0], 0) != hipSuccess) return fail(WG_EHIP, "fork wait failed");
     // step s of every range is issued before step s + 1 of any: the ranges start together and stay side by side in
     // the hardware queues (range by range, the second range would start only after the host had issued all of the
-    // first range's launches)
-    for (int s = 0; s < n_steps; s++)
-        for (int i = 0; i < n; i++) {
-            const wg_range &r = ranges[i];
-            const int rc = run(r.batch, p, action ? action + r.action_offset : nullptr, action_cols, action_stride,
-                               action_step, r.outputs, 1, r.plan, r.plan_blocks, r.stream, true, false, false, s);
-            if (rc) return rc;
+    // first range's launches).  WG_RANGE_LEAD: range 0's first `lead` steps issued before the others' first;
+    // WG_RANGE_SKEW_US: range i starts i * skew us after range 0 (range_skew_kernel)
+    const int lead = std::min(std::max(env_int("WG_RANGE_LEAD", 0), 0), (int)n_steps);
+    const long long skew = n_steps > 1 ? std::min(std::max(env_int("WG_RANGE_SKEW_US", 0), 0), 200) * 100ll : 0;
+    auto issue = [&](int i, int s) -> int {
+        const wg_range &r = ranges[i];
+        if (s == 0 && i > 0 && skew > 0) {
+            hipLaunchKernelGGL(range_skew_kernel, dim3(1), dim3(64), 0, r.stream, skew * i);
+            if (hipGetLastError() != hipSuccess) return fail(WG_EHIP, "skew launch failed");
         }
+        return run(r.batch, p, action ? action + r.action_offset : nullptr, action_cols, action_stride, action_step,
+                   r.outputs, 1, r.plan, r.plan_blocks, r.stream, true, false, false, s);
+    };
+    for (int s = 0; s < lead; s++)
+        if (const int rc = issue(0, s)) return rc;
+    for (int s = 0; s < n_steps; s++) {
+        for (int i = 1; i < n; i++)
+            if (const int rc = issue(i, s)) return rc;
+        if (s + lead < n_steps)
+            if (const int rc = issue(0, s + lead)) return rc;
+    }
     for (int i = 1; i < n; i++)
         if (hipEventRecord(events[i], ranges[i].stream) != hipSuccess || hipStreamWaitEvent(s0, events[i], 0) != hipSuccess)
             return fail(WG_EHIP, "join event failed");

@@ -82,13 +82,14 @@ def require_tensor(t, name: str, device, dtype, shape=None) -> None:
     GPU), another dtype, a non-contiguous layout or a wrong shape.  Raises ValueError before any launch."""
     if not isinstance(t, torch.Tensor):
         raise ValueError(f"{name} must be a torch tensor on {device}")
-    if t.device != torch.device(device):
+    # (on the per-call path of run(): `torch.device.__ne__` and tuple(t.shape) cost microseconds each, == does not)
+    if not (t.device == (device if isinstance(device, torch.device) else torch.device(device))):
         raise ValueError(f"{name} is on {t.device}, the batch is on {device}")
     if t.dtype != dtype:
         raise ValueError(f"{name} has dtype {t.dtype}, expected {dtype}")
     if not t.is_contiguous():
         raise ValueError(f"{name} must be contiguous")
-    if shape is not None and tuple(t.shape) != tuple(shape):
+    if shape is not None and not (t.shape == (shape if isinstance(shape, tuple) else tuple(shape))):
         raise ValueError(f"{name} has shape {tuple(t.shape)}, expected {tuple(shape)}")
 
 

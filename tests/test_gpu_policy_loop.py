@@ -47,15 +47,46 @@ def test_policy_loop_equals_step_loop(lanes, graph):
     assert not torch.equal(acts_seen[1], acts_seen[T - 1])
 
 
-def test_policy_loop_refuses_ragged_and_bad_actions():
+@pytest.mark.parametrize("kind,lanes,graph", [("ragged", 1, False), ("ragged", 2, False), ("ragged", 3, True),
+                                              ("lattice25", 2, False)])
+def test_policy_loop_ragged_equals_step_loop(kind, lanes, graph):
+    """Mixed-topology batches (stored in wave-tile order) and uniform M = 25 walkers (wave tiles in
+    identity order): each range gathers its caller rows, applies the policy, scatters the actions; the trajectories
+    are bit-identical to `for t: step(policy(obs, t))`."""
     import torch
+    from walker_gym_amd.batched_env import BatchedPhysicsEnv
+    from walker_gym_amd.synthetic import canonical_walkers, ragged_walkers
+    N, T = 3000, 10
+    spec = ragged_walkers(N, seed=41, mmin=4, mmax=32) if kind == "ragged" else canonical_walkers(N, seed=5, M=25, K=60,
+                                                                                                  A=10)
+    ref = BatchedPhysicsEnv(spec, device="cuda:0", in3d=1)
+    W = torch.randn((ref.obs_dim, 12), generator=torch.Generator().manual_seed(4)).cuda() * 0.05
+
+    def policy(rows, t):
+        return torch.tanh(rows @ W + 0.01 * t)
+
+    assert ref.batch.ragged and ref.batch.plan_blocks >= 3 * 64
+    for t in range(T):
+        ref.step(policy(ref.obs, t))
+    env = BatchedPhysicsEnv(spec, device="cuda:0", in3d=1)
+    env.policy_loop(policy, T, lanes=lanes, graph=graph)
+    torch.cuda.synchronize()
+    for name in ("pos", "vel", "acc", "obs", "reward", "done", "centroid", "energy", "muscle_x"):
+        assert np.array_equal(_bits(getattr(env, name)), _bits(getattr(ref, name))), name
+    assert torch.equal(env.steps, ref.steps)
+    assert torch.equal(env.info()["steps"], ref.info()["steps"])
+
+
+def test_policy_loop_refuses_bad_actions():
     from walker_gym_amd.batched_env import BatchedPhysicsEnv
     from walker_gym_amd.synthetic import canonical_walkers, ragged_walkers
     rg = BatchedPhysicsEnv(ragged_walkers(200, seed=2), device="cuda:0", in3d=1)
     with pytest.raises(ValueError):
-        rg.policy_loop(lambda rows, t: rows[:, :4].contiguous(), 2)
+        rg.policy_loop(lambda rows, t: rows[:3, :4].contiguous(), 2)
     env = BatchedPhysicsEnv(canonical_walkers(256, seed=2), device="cuda:0", in3d=1)
     with pytest.raises(ValueError):
         env.policy_loop(lambda rows, t: rows[:5, :8].contiguous(), 1)
     with pytest.raises(ValueError):
         env.policy_loop(lambda rows, t: rows[:, :8].double(), 1)
+    with pytest.raises(ValueError):   # a later step returning another shape is refused before its launch
+        env.policy_loop(lambda rows, t: rows[:, :8 if t == 0 else 6].contiguous(), 3)

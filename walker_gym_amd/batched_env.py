@@ -104,6 +104,7 @@ class WalkerGraph:
         self.actions = actions            # kept alive: the graph reads it on every replay
         # the replayed steps write info['steps'] in caller order (env.steps_out) only when captured with info
         self._writes_steps = bool(info) and env.steps_out is not None
+        self._stale = frozenset() if info else frozenset({"centroid_position", "total_energy", "momentum", "nonfinite"})
 
     def replay(self) -> None:
         env = self._env
@@ -114,6 +115,31 @@ class WalkerGraph:
         # the batch's step counters moved: steps_out is current only if the graph wrote it (a graph
         # captured with info=False left a step()'s steps_out looking valid)
         env._steps_at = env.batch.version if self._writes_steps else -1
+        env._stale = self._stale
+
+
+class PreparedRun:
+    """run()'s C call with its arguments already built (BatchedPhysicsEnv.prepare_run): calling it issues the prepared
+    steps again.  Like a WalkerGraph it refuses to run once the env's parameters or buffers have changed."""
+
+    def __init__(self, env: "BatchedPhysicsEnv", entry: str, fn, args, keep, steps_valid: bool, stale: set,
+                 thunk=None):
+        self._env, self._gen, self._struct = env, env._generation, env.batch.struct
+        self._entry, self._fn, self._args, self._keep, self._thunk = entry, fn, args, keep, thunk
+        self._steps_valid, self._stale = steps_valid, frozenset(stale)
+
+    def __call__(self) -> None:
+        env = self._env
+        if env._generation != self._gen or env.batch.struct is not self._struct:
+            raise RuntimeError("stale PreparedRun: the env's parameters or buffers changed after prepare_run")
+        if self._thunk is not None:
+            self._thunk(*self._args)
+        else:
+            rc = self._fn(*self._args)
+            if rc:
+                _lib.check(rc, self._entry)
+        env._steps_at = env.batch.version if self._steps_valid else -1
+        env._stale = self._stale
 
 
 class BatchedPhysicsEnv:
@@ -142,6 +168,7 @@ class BatchedPhysicsEnv:
         if seed is not None:
             self._gen.manual_seed(int(seed))
         self._generation = 0
+        self._stale = frozenset()   # info() keys the last run() did not write (record buffers / info=False)
         # opt-in info (ABI 10): info['momentum'] (Point.momentum per walker, gym/engine.py:160-166) and
         # info['nonfinite'] (a walker whose state holds an inf / NaN; done is left as the reference computes it)
         self._extras = bool(info_extras)
@@ -199,10 +226,14 @@ class BatchedPhysicsEnv:
 
     def enable_info_extras(self) -> None:
         """Start producing info['momentum'] and info['nonfinite'] every step (one small per-walker pass after the
-        step kernel).  Graphs captured before this raise on replay (the outputs were reallocated)."""
+        step kernel).  The other output tensors stay the same objects; graphs captured before this raise on replay."""
         if not self._extras:
+            # only the two new buffers (ADVICE r4: reallocating every output silently detached the tensors a caller
+            # still held from step()); the generation bump makes cached plans and graphs rebuild / refuse
             self._extras = True
-            self._alloc_outputs()
+            self.momentum = torch.zeros((self.N, 3), dtype=torch.float32, device=self.device)
+            self.nonfinite = torch.zeros(self.N, dtype=torch.bool, device=self.device)
+            self._generation += 1
 
     def _outputs(self, obs=None, reward=None, done=None, centroid=None, energy=None, obs_step=0, out_step=0,
                  pad_clean=False, steps=None, nonfinite=None, momentum=None):
@@ -299,6 +330,7 @@ class BatchedPhysicsEnv:
         if rc:
             _lib.check(rc, "wg_step_ranges")
         self._steps_at = self.batch.version
+        self._stale = frozenset()
         if act is not None and plan["n"] > 1 and not torch.cuda.is_current_stream_capturing():
             for st in plan["side"]:
                 act.record_stream(st)   # the allocator must not recycle the actions before the side streams read them
@@ -366,6 +398,8 @@ class BatchedPhysicsEnv:
         T, _, cols = actions.shape
         dv = self.device
         self._steps_at = -1   # the step counters move without the steps output: info() gathers them afterwards
+        # (the per-step outputs went to the rollout's buffers: the env's own centroid / energy / extras are not current)
+        self._stale = frozenset({"centroid_position", "total_energy", "momentum", "nonfinite"})
         # zero-filled: a ragged batch's short rows then need only their own values written each step
         clean = obs_out is None
         obs_out = torch.zeros((T, self.N, self.obs_dim), dtype=torch.float32, device=dv) if obs_out is None else obs_out
@@ -400,7 +434,19 @@ class BatchedPhysicsEnv:
         record: every step's reward / done (and with info, energy / centroid) into caller buffers instead of the
         env's one-step outputs — {'reward': [n_steps, N] f32, 'done': [n_steps, N] bool or u8, optionally 'energy'
         [n_steps, N] f32 and 'centroid' [n_steps, N, 3] f32} — while obs keeps the last step's rows (env.obs): the
-        rollout SURVEY §8(e) gathers at its end.  The same bytes as a plain run, written at per-step offsets."""
+        rollout SURVEY §8(e) gathers at its end.  The same bytes as a plain run, written at per-step offsets.  After a
+        record run env.reward / done / centroid / energy and the info extras are not this run's (they went to the
+        record buffers, or were not computed): info() leaves those keys out until the next step() / observe() / run()
+        without record."""
+        self.prepare_run(actions, n_steps, info=info, lanes=lanes, resident=resident, record=record)()
+
+    def prepare_run(self, actions, n_steps: int, info: bool = True, lanes: Optional[int] = None,
+                    resident: bool = False, record: Optional[dict] = None) -> "PreparedRun":
+        """run()'s argument checks, walker ranges and C structs, built once: the returned PreparedRun issues the same
+        n_steps steps with ONE C call each time it is called (on the stream that was current here), so the host time
+        between a caller's clock start and the first launch is one ctypes call (bench.py builds it before its timed
+        region: ~35 us of Python before the first launch otherwise).  It holds raw pointers to `actions`,
+        the record buffers and the env's tensors: set_params / a reallocation of the outputs make it raise."""
         require_tensor(actions, "actions", self.device, torch.float32)
         if actions.dim() != 3:
             raise ValueError("actions must be a contiguous [n_steps or 1, N, A] device tensor")
@@ -411,8 +457,12 @@ class BatchedPhysicsEnv:
         entry = "wg_rollout" if resident else "wg_step"
         so = self.steps_out if info else None
         rew, done, cen, en, out_step = self.reward, self.done, self.centroid, self.energy, 0
+        stale = set()
         if record is not None:
             S = int(n_steps)
+            if S < 1:
+                raise ValueError("run(record=...) needs n_steps >= 1")
+            stale = {"centroid_position", "total_energy", "momentum", "nonfinite"}
             rew, done = record["reward"], record["done"]
             require_tensor(rew, "record['reward']", self.device, torch.float32, (S, self.N))
             if not isinstance(done, torch.Tensor) or done.dtype not in (torch.bool, torch.uint8):
@@ -428,21 +478,30 @@ class BatchedPhysicsEnv:
             so, out_step = None, self.N   # (the steps output would need [n_steps, N] too: info() gathers them)
         if not info:
             cen = en = None
+            stale |= {"centroid_position", "total_energy", "momentum", "nonfinite"}
         # the opt-in info extras follow the last step only when the outputs are overwritten each step (no record)
         o = self._outputs(self.obs, rew, done, cen, en, pad_clean=True, steps=so, out_step=out_step,
                           **(self._extra_out() if (info and record is None) else {}))
+        steps_valid = so is not None
+        n_steps = int(n_steps)
         if lanes > 1:
-            self._run_lanes(actions, int(n_steps), o, lanes, entry=entry)
-            self._steps_at = self.batch.version if so is not None else -1
-            return
-        _lib.check(getattr(_lib.load(), entry)(
-            C.byref(self.batch.struct), C.byref(self._pstruct), C.c_void_p(actions.data_ptr()), cols, cols,
-            0 if T == 1 else self.N * cols, C.byref(o), int(n_steps),
-            None if self.batch.plan is None else C.c_void_p(self.batch.plan.data_ptr()),
-            self.batch.plan_blocks, self._stream()), entry)
+            capturing = torch.cuda.is_current_stream_capturing()
+            if entry == "wg_step" and not capturing and os.environ.get("WG_RANGE_ISSUE", "inter") != "seq":
+                fn, args, keep = self._run_ranges_args(actions, n_steps, o, lanes)
+                if n_steps > 0:
+                    for st in self._side[:lanes - 1]:
+                        actions.record_stream(st)   # the allocator must not recycle it before the side streams are done
+                return PreparedRun(self, "wg_run_ranges", fn, args, keep, steps_valid, stale)
+            # (range-by-range issue, a resident rollout over several ranges, or a graph capture: one C call per range)
+            return PreparedRun(self, entry, None, (actions, n_steps, o, lanes, entry), [o], steps_valid, stale,
+                               thunk=self._run_lanes)
         # (a resident launch writes the steps output only where the resident kernel runs: uniform batches, which
         # have no steps_out)
-        self._steps_at = self.batch.version if so is not None else -1
+        args = (C.byref(self.batch.struct), C.byref(self._pstruct), actions.data_ptr(), cols, cols,
+                0 if T == 1 else self.N * cols, C.byref(o), n_steps,
+                None if self.batch.plan is None else self.batch.plan.data_ptr(), self.batch.plan_blocks,
+                torch.cuda.current_stream(self.device).cuda_stream)
+        return PreparedRun(self, entry, getattr(_lib.load(), entry), args, [o, actions], steps_valid, stale)
 
     def _lanes(self, lanes: Optional[int]) -> int:
         """Walker ranges run() steps on separate streams (ragged batches: ranges of plan blocks).  Default 2 for
@@ -487,8 +546,45 @@ class BatchedPhysicsEnv:
             cached = self._range_cache = (key, st, [self.batch.sub_struct(bounds[i], bounds[i + 1]) for i in range(lanes)])
         return cached[2]
 
+    def _range_bounds(self, lanes: int) -> list:
+        """Walker ranges of run(): plan-block bounds (ragged: the same batch, a slice of its block -> walker plan) or
+        walker bounds on multiples of 64 (uniform)."""
+        if self.batch.ragged:
+            nb = self.batch.plan_blocks
+            return [nb * i // lanes for i in range(lanes)] + [nb]
+        return [0] + [((self.N * i // lanes) + 63) // 64 * 64 for i in range(1, lanes)] + [self.N]
+
+    def _run_ranges_args(self, actions, n_steps: int, o_full, lanes: int):
+        """wg_run_ranges' arguments for n_steps of `lanes` walker ranges on the calling stream and the side streams:
+        step s of every range is issued before step s + 1 of any (WG_RANGE_ISSUE=seq keeps range-by-range issue, one
+        wg_step call each: the last range then starts only after the host has issued every launch of the ranges
+        before it; scripts/issue_ab.sh).  Returns (function, arguments, the ctypes objects they point at)."""
+        T, n, cols = actions.shape
+        cur = torch.cuda.current_stream(self.device)
+        self.reserve_streams(lanes)
+        ragged = self.batch.ragged
+        bounds = self._range_bounds(lanes)
+        rng, keep = (_lib.WgRange * lanes)(), []
+        subs = None if ragged else self._range_batches(lanes, bounds)
+        for i in range(lanes):
+            w0, w1 = bounds[i], bounds[i + 1]
+            if ragged:
+                o, rng[i].batch, rng[i].action_offset = o_full, C.pointer(self.batch.struct), 0
+                rng[i].plan, rng[i].plan_blocks = self.batch.plan.data_ptr() + 4 * w0, w1 - w0
+            else:
+                o, rng[i].batch, rng[i].action_offset = self._range_outputs(o_full, w0), C.pointer(subs[i]), w0 * cols
+                rng[i].plan, rng[i].plan_blocks = None, 0
+            keep.append(o)
+            rng[i].outputs = C.pointer(o)
+            rng[i].stream = (cur if i == 0 else self._side[i - 1]).cuda_stream
+        keep += [rng, o_full, actions, subs]
+        args = (rng, lanes, C.byref(self._pstruct), actions.data_ptr(), cols, cols, 0 if T == 1 else self.N * cols,
+                n_steps, self._range_events(lanes))
+        return _lib.load().wg_run_ranges, args, keep
+
     def _run_lanes(self, actions, n_steps: int, o_full, lanes: int, entry: str = "wg_step"):
-        """n_steps with the walkers split into `lanes` contiguous ranges, each stepped by its own stream: the
+        """n_steps with the walkers split into `lanes` contiguous ranges, each stepped by its own stream, one C call
+        per range (the range-by-range form; prepare_run issues the ranges step by step through wg_run_ranges): the
         ranges are independent, so one range's step t + 1 fills the GPU while another's step t drains (the
         launch tail).  Every walker still takes every step, one launch per step per range; the calling
         stream waits for all ranges before returning (stream-ordered, no host sync).  o_full: the whole batch's
@@ -498,35 +594,8 @@ class BatchedPhysicsEnv:
         self.reserve_streams(lanes)
         L = _lib.load()
         ragged = self.batch.ragged
-        if ragged:   # ranges of plan blocks: the same batch, a slice of its block -> walker plan
-            nb = self.batch.plan_blocks
-            bounds = [nb * i // lanes for i in range(lanes)] + [nb]
-        else:
-            bounds = [0] + [((self.N * i // lanes) + 63) // 64 * 64 for i in range(1, lanes)] + [self.N]
+        bounds = self._range_bounds(lanes)
         capturing = torch.cuda.is_current_stream_capturing()
-        if entry == "wg_step" and not capturing and os.environ.get("WG_RANGE_ISSUE", "inter") != "seq":
-            # one wg_run_ranges call: step s of every range issued before step s + 1 of any (WG_RANGE_ISSUE=seq:
-            # range by range, one wg_step call each: the last range starts only after the host has issued every
-            # launch of the ranges before it; scripts/issue_ab.sh)
-            rng, keep = (_lib.WgRange * lanes)(), []
-            subs = None if ragged else self._range_batches(lanes, bounds)
-            for i in range(lanes):
-                w0, w1 = bounds[i], bounds[i + 1]
-                if ragged:
-                    o, rng[i].batch, rng[i].action_offset = o_full, C.pointer(self.batch.struct), 0
-                    rng[i].plan, rng[i].plan_blocks = self.batch.plan.data_ptr() + 4 * w0, w1 - w0
-                else:
-                    o, rng[i].batch, rng[i].action_offset = self._range_outputs(o_full, w0), C.pointer(subs[i]), w0 * cols
-                    rng[i].plan, rng[i].plan_blocks = None, 0
-                keep.append(o)
-                rng[i].outputs = C.pointer(o)
-                rng[i].stream = (cur if i == 0 else self._side[i - 1]).cuda_stream
-            _lib.check(L.wg_run_ranges(rng, lanes, C.byref(self._pstruct), C.c_void_p(actions.data_ptr()), cols, cols,
-                                       0 if T == 1 else self.N * cols, n_steps, self._range_events(lanes)),
-                       "wg_run_ranges")
-            for st in self._side[:lanes - 1]:
-                actions.record_stream(st)   # the allocator must not recycle it before the side streams are done
-            return
         start = torch.cuda.Event()
         start.record(cur)
         done = []
@@ -576,51 +645,106 @@ class BatchedPhysicsEnv:
         stream.  It must be row-wise — walker w's action a function of walker w's observation only — which is what
         makes the ranges independent; then the results are bit-identical to `for t: env.step(policy(env.obs, t))`.
         graph=True captures the n_steps x ranges loop (policy kernels included) as one HIP graph and replays it once
-        (no per-step host cost; the policy must be capturable).  Uniform batches (a ragged range's rows are not
-        contiguous in the caller's order).  After the call obs / reward / done / info hold the last step's outputs."""
-        if self.batch.ragged:
-            raise ValueError("policy_loop: uniform batches only (a ragged walker range is not a row slice)")
+        (no per-step host cost; the policy must be capturable).  After the call obs / reward / done / info hold the last
+        step's outputs.
+
+        Ragged batches (stored in wave-tile order, wg_batch.row) run ranges of plan blocks, whose walkers are a
+        scattered set of caller rows: each range gathers its rows of obs (index_select), applies the policy to them and
+        scatters the actions into its rows of one [N, A] action buffer (index_copy_), which its step reads by caller
+        row; the ranges' rows are disjoint, so they still never wait for one another.
+
+        Host cost per range and step (what bounds a small batch's loop): the policy's own launches, a shape / dtype
+        check against the first step's actions, and one C call; the stream is switched only when there are several
+        ranges (one range runs on the calling stream as it is)."""
+        b = self.batch
         lanes = self._lanes(lanes)
-        bounds = [0] + [((self.N * i // lanes) + 63) // 64 * 64 for i in range(1, lanes)] + [self.N]
         self.reserve_streams(lanes)
         L = _lib.load()
-        ranges = []
-        for i in range(lanes):
-            w0, w1 = bounds[i], bounds[i + 1]
-            sub = self.batch.sub_struct(w0, w1)
-            o = self._outputs(self.obs[w0:w1], self.reward[w0:w1], self.done[w0:w1], self.centroid[w0:w1],
-                              self.energy[w0:w1], pad_clean=True, **self._extra_out(w0, w1))
-            ranges.append((w0, w1, sub, o))
-        # the per-step host work is what a policy loop's rate is bound by (two ranges x (policy + step) per env step
-        # against a 34 us step): the range's obs view and the C arguments are built once, not per step
         pref, dev, f32 = C.byref(self._pstruct), self.device, torch.float32
-        args = [(self.obs[w0:w1], w1 - w0, C.byref(sub), C.byref(o)) for (w0, w1, sub, o) in ranges]
+        args = []   # per range: (obs rows or None, row index or None, n_r, batch ref, outputs ref, plan ptr, blocks)
+        keep = []   # the ctypes structs the refs point at
+        plan_rows = []   # ragged: the stored walker range [s0, s1) of each range
+        if b.ragged:
+            nb = b.plan_blocks
+            bb = [nb * i // lanes for i in range(lanes)] + [nb]
+            o = self._outputs(self.obs, self.reward, self.done, self.centroid, self.energy, pad_clean=True,
+                              steps=self.steps_out, **self._extra_out())
+            keep.append(o)
+            for i in range(lanes):
+                s0, s1 = int(b.plan_host[bb[i]]), int(b.plan_host[bb[i + 1]])
+                plan_rows.append((s0, s1))
+                if b.row is None:   # identity order (uniform walkers of M not dividing 64): a row slice
+                    obs_r, idx = self.obs[s0:s1], None
+                else:               # the caller rows of stored walkers s0 .. s1 - 1
+                    obs_r, idx = None, b._perm["row"][s0:s1]
+                args.append((obs_r, idx, s1 - s0, C.byref(b.struct), C.byref(o),
+                             C.c_void_p(b.plan.data_ptr() + 4 * bb[i]), bb[i + 1] - bb[i]))
+        else:
+            bounds = [0] + [((self.N * i // lanes) + 63) // 64 * 64 for i in range(1, lanes)] + [self.N]
+            for i in range(lanes):
+                w0, w1 = bounds[i], bounds[i + 1]
+                sub = b.sub_struct(w0, w1)
+                o = self._outputs(self.obs[w0:w1], self.reward[w0:w1], self.done[w0:w1], self.centroid[w0:w1],
+                                  self.energy[w0:w1], pad_clean=True, **self._extra_out(w0, w1))
+                keep += [sub, o]
+                args.append((self.obs[w0:w1], None, w1 - w0, C.byref(sub), C.byref(o), None, 0))
+        def check(a, n_r):
+            require_tensor(a, "policy actions", dev, f32)
+            if a.dim() != 2 or a.shape[0] != n_r:
+                raise ValueError(f"policy returned {tuple(a.shape)}, expected [{n_r}, A]")
 
         def body(cur):
             streams = [cur] + self._side[:lanes - 1]
-            start = torch.cuda.Event()
-            start.record(cur)
-            for st in streams[1:]:
-                st.wait_event(start)
+            if lanes > 1:
+                start = torch.cuda.Event()
+                start.record(cur)
+                for st in streams[1:]:
+                    st.wait_event(start)
             step = L.wg_step
-            sts = [(st, C.c_void_p(st.cuda_stream)) for st in streams]
-            for t in range(int(n_steps)):
-                for (obs_r, n_r, sub_ref, o_ref), (st, st_ptr) in zip(args, sts):
-                    with torch.cuda.stream(st):
-                        a = policy(obs_r, t)
-                        require_tensor(a, "policy actions", dev, f32)
-                        if a.dim() != 2 or a.shape[0] != n_r:
-                            raise ValueError(f"policy returned {tuple(a.shape)}, expected [{n_r}, A]")
+            sts = [(st, st.cuda_stream) for st in streams]
+            shapes = [None] * lanes
+            dix = dev.index
+            abuf = None   # ragged: the [N, A] action buffer the ranges scatter into (allocated at the first step, on
+            #               the calling stream, which every range's stream joins at the end)
+            try:
+                for t in range(int(n_steps)):
+                    for r, ((obs_r, idx, n_r, b_ref, o_ref, plan, nblk), (st, st_ptr)) in enumerate(zip(args, sts)):
+                        if lanes > 1:
+                            torch.cuda.set_stream(st)
+                        a = policy(obs_r if idx is None else self.obs.index_select(0, idx), t)
+                        # the full check at a range's first step, then the same shape, dtype, device and layout
+                        if shapes[r] is None:
+                            check(a, n_r)
+                            if r > 0 and a.shape[1] != shapes[0][1]:
+                                raise ValueError("policy actions: every walker range must return the same columns")
+                            shapes[r] = a.shape
+                        elif not (a.shape == shapes[r] and a.dtype == f32 and a.get_device() == dix and
+                                  a.is_contiguous()):
+                            check(a, n_r)
+                            raise ValueError(f"policy actions changed shape: {tuple(a.shape)} after "
+                                             f"{tuple(shapes[r])}")
                         cols = a.shape[1]
-                        rc = step(sub_ref, pref, a.data_ptr(), cols, cols, 0, o_ref, 1, None, 0, st_ptr)
+                        if plan is not None:   # ragged: the range's caller rows of the action buffer
+                            if abuf is None:
+                                abuf = torch.zeros((self.N, cols), dtype=f32, device=dev)
+                            if idx is None:
+                                abuf[plan_rows[r][0]:plan_rows[r][1]].copy_(a)
+                            else:
+                                abuf.index_copy_(0, idx, a)
+                            a = abuf
+                        rc = step(b_ref, pref, a.data_ptr(), cols, cols, 0, o_ref, 1, plan, nblk, st_ptr)
                         if rc:
                             _lib.check(rc, "wg_step")
+            finally:
+                if lanes > 1:
+                    torch.cuda.set_stream(cur)
             for st in streams[1:]:
                 ev = torch.cuda.Event()
                 ev.record(st)
                 cur.wait_event(ev)
 
         self._steps_at = -1
+        self._stale = frozenset()
         if not graph:
             body(torch.cuda.current_stream(self.device))
             return
@@ -644,12 +768,12 @@ class BatchedPhysicsEnv:
         g = torch.cuda.CUDAGraph()
         side = torch.cuda.Stream(device=self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
-        steps_at = self._steps_at               # capture runs nothing: the outputs' validity is unchanged by it
+        steps_at, stale = self._steps_at, self._stale   # capture runs nothing: the outputs' validity is unchanged
         with torch.cuda.stream(side):           # capture off the default stream, as torch requires
             with torch.cuda.graph(g, stream=side):
                 self.run(actions, n_steps, info=info, lanes=lanes)
         torch.cuda.current_stream(self.device).wait_stream(side)
-        self._steps_at = steps_at
+        self._steps_at, self._stale = steps_at, stale
         return WalkerGraph(self, g, actions, info=info)
 
     def observe(self):
@@ -660,6 +784,7 @@ class BatchedPhysicsEnv:
             None if self.batch.plan is None else C.c_void_p(self.batch.plan.data_ptr()),
             self.batch.plan_blocks, self._stream()), "wg_observe")
         self._steps_at = self.batch.version
+        self._stale = frozenset()
         return self.obs, self.reward, self.done, self.info()
 
     def reset(self, noise=None, mask=None):
@@ -692,6 +817,8 @@ class BatchedPhysicsEnv:
         if self._extras:
             info["momentum"] = self.momentum      # Point.momentum (gym/engine.py:160-166) of each walker
             info["nonfinite"] = self.nonfinite    # True: the walker's pos / vel / acc hold an inf or NaN
+        for k in self._stale:                     # not written by the last run() (record buffers, info=False)
+            info.pop(k, None)
         return info
 
     # state accessors in the caller's order.  An unpermuted batch returns live views into its tensors; a ragged batch

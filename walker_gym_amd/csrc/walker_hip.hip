@@ -48,13 +48,12 @@ int fail(int code, const char *fmt, ...) {
 constexpr int WG_MAX_M = 1024;      // numpy pairwise recursion unrolled 3 levels (pw_tree<3>)
 constexpr double CONFIG_R = 16e-36;  // gym/engine.py:9 Config.r (distance clamp, Python float)
 constexpr int EPL = 4;               // edges per lane per pass held in registers
-#ifndef WG_NTHREADS
-#define WG_NTHREADS 256
-#endif
-constexpr int NTHREADS = WG_NTHREADS;   // default workgroup size (walkers fill 256 mass lanes)
+constexpr int NTHREADS = 256;           // default workgroup size (walkers fill 256 mass lanes)
 constexpr int MAXT = 512;               // __launch_bounds__: workgroups are 64..512 threads (> 256: M > 64 only)
+// Diagnostic builds only (scripts/variant_ab.py, -DWG_ABLATE=bits): bit k skips phase k of the step to price it.  Such a
+// build's results are NOT exact (tests/test_abi.py compiles one; no GPU test loads it); 0 in the product.
 #ifndef WG_ABLATE
-#define WG_ABLATE 0   // profiling builds only (scripts/variant_ab.py): bit k skips phase k; 0 in the product
+#define WG_ABLATE 0
 #endif
 
 // Float32 constants derived from wg_params exactly where numpy rounds the Python scalars.
@@ -309,12 +308,6 @@ __device__ inline float fdiv_exact(float x, double y) { return (float)((double)x
 // double product rounded to a subnormal float can sit on a rounding midpoint.  fexp is frexp's exponent (0 for 0,
 // inf and NaN: zero dividends pass), so one min over fexp's tests a whole set of dividends.
 constexpr int TINY_EXP = -79;   // fexp(x) >= TINY_EXP  <=>  x == 0 or |x| >= 2^-80
-#ifndef WG_DUAL_SUM
-#define WG_DUAL_SUM 1   // wave kernel: the reduction lanes' sequential and pairwise sums in one interleaved path
-#endif
-#ifndef WG_GUARDS
-#define WG_GUARDS 15   // diagnostic builds only (cost A/B, results not exact): bit 1 spring dividends, 2 damping
-#endif                 // forces, 4 env dividends, 8 mass range; the product keeps all four
 __device__ __forceinline__ int fexp(float x) { return __builtin_amdgcn_frexp_expf(x); }
 __device__ __forceinline__ int fexp3(float a, float b, float c) { return min(min(fexp(a), fexp(b)), fexp(c)); }
 __device__ __forceinline__ bool divisor_ok(float m) {   // m in [2^-20, 2^21) in magnitude
@@ -379,14 +372,10 @@ __device__ __forceinline__ double rcp64_nr(double d) {
 // the range, both signs (scripts/check_rcp64.hip, profiles/r04_rcp64_exhaustive.json) — 5 VALU instead of the ~12 of
 // the IEEE division, and a shorter dependent chain; any other m (0, subnormal, inf, NaN, outside the range) takes the
 // IEEE division, so the guarded paths see exactly what they saw before.
-#ifndef WG_YM_RCP
-#define WG_YM_RCP 1
-#endif
 __device__ __forceinline__ double rcp64_nr(double d);
 __device__ __forceinline__ bool divisor_ok(float m);
 __device__ __forceinline__ double recip_m(float mf) {
     const double md = (double)mf;
-    if (!WG_YM_RCP) return 1.0 / md;
     double y = rcp64_nr(md);
     if (__builtin_expect(!divisor_ok(mf), 0)) y = 1.0 / md;
     return y;
@@ -399,11 +388,7 @@ __device__ __forceinline__ double recip_m(float mf) {
 // division would.  |x| < 2^-100 (a possibly subnormal quotient, where that spacing argument fails) takes the
 // IEEE division, in a branch.  3 VALU instead of the ~11 of a correctly rounded float32 division.  Checked on the
 // host for M < 2^11 with reciprocals up to two ulps off (scripts/check_division.c, tests/test_exact_division.py).
-#ifndef WG_FAST_MEAN
-#define WG_FAST_MEAN 1
-#endif
 __device__ __forceinline__ float fdiv_count(float x, float fM, double yM) {
-    if (!WG_FAST_MEAN) return x / fM;
     float q = (float)((double)x * yM);
     if (__builtin_expect(__builtin_fabsf(x) < 0x1p-100f, 0)) q = x / fM;
     return q;
@@ -416,13 +401,10 @@ __device__ __attribute__((noinline)) float np_sq_cold(float x) { return pw_pow2(
 // INL: the restated powf inline instead of a call — the latency-bound small-tile instances (lean NE = 1: a launch lasts
 // as long as its slowest wave, and ~10 % of waves take this path): Balance-4096 -1.6 %, while the large tiles keep the
 // call (canonical +1.0 % inline; profiles/r03zq_ab_sqinl_*.txt)
-#ifndef WG_SQ_COLD
-#define WG_SQ_COLD 1   // 0: timing builds only (results not exact): RN(x*x) everywhere, to price the cold path
-#endif
 template <bool INL = false>
 __device__ __forceinline__ float np_sq(float x) {
     float f;
-    if (__builtin_expect(!pw_pow2_fast(x, &f), 0) && WG_SQ_COLD) f = INL ? pw_pow2(x) : np_sq_cold(x);
+    if (__builtin_expect(!pw_pow2_fast(x, &f), 0)) f = INL ? pw_pow2(x) : np_sq_cold(x);
     return f;
 }
 // The workgroup kernel's copy of glibc's powf tables in LDS (filled by its first 32 threads before its first barrier):
@@ -431,25 +413,13 @@ __device__ __forceinline__ float np_sq(float x) {
 // cold path: with the global tables it cost 21 % of the launch (188.5 against 149.6 us with RN(x*x) everywhere,
 // profiles/r04y_ab_perfdemo_sq.json).  pw_pow2's arithmetic, unchanged (powf2.h); checked on the GPU against pw_pow2
 // for every float32 bit pattern (scripts/check_pow2_lanes.hip).
-#ifndef WG_SQ_LDS
-#define WG_SQ_LDS 1
-#endif
 __shared__ double s_pw_log2[32];
 __shared__ unsigned long long s_pw_exp2[32];
 __device__ __forceinline__ void pw_tables_to_lds(int tid) {
     if (tid < 32) { s_pw_log2[tid] = PW_LOG2_TAB[tid]; s_pw_exp2[tid] = PW_EXP2_TAB[tid]; }
 }
-#ifndef WG_SQ_LDS_INL
-#define WG_SQ_LDS_INL 1   // the LDS-table evaluation inline in the pair loop (0: a call; 186.9 against 183.5 us perfdemo)
-#endif
-template <bool INL>
-__device__ __forceinline__ float pw_pow2_lds_body(float x);
-__device__ __attribute__((noinline)) float pw_pow2_lds_call(float x) { return pw_pow2_lds_body<false>(x); }
+// (evaluated inline in the pair loop: a call ran 186.9 against 183.5 us perfdemo)
 __device__ __forceinline__ float pw_pow2_lds(float x) {
-    return WG_SQ_LDS_INL ? pw_pow2_lds_body<true>(x) : pw_pow2_lds_call(x);
-}
-template <bool INL>
-__device__ __forceinline__ float pw_pow2_lds_body(float x) {
     unsigned int ix = pw_asu32(x) & 0x7fffffffu;
     if (ix == 0u || ix >= 0x7f800000u) return x * x;
     if (ix < 0x00800000u) {
@@ -490,18 +460,11 @@ __device__ __forceinline__ float pw_pow2_lds_body(float x) {
     return (float)(yy * sc);
 }
 // np_sq with the cold path on the LDS tables (workgroup kernel only: the tables must have been filled)
-#if WG_SQ_COLD == 2
-__device__ int g_sq_never;   // (timing builds: a cold path the compiler must keep but the run never takes)
-#endif
 template <bool LDS_TAB>
 __device__ __forceinline__ float np_sq_t(float x) {
-    if (!(LDS_TAB && WG_SQ_LDS)) return np_sq(x);
+    if (!LDS_TAB) return np_sq(x);
     float f;
-#if WG_SQ_COLD == 2
-    if (__builtin_expect(!pw_pow2_fast(x, &f), 0) && __builtin_nontemporal_load(&g_sq_never)) f = pw_pow2_lds(x);
-#else
-    if (__builtin_expect(!pw_pow2_fast(x, &f), 0) && WG_SQ_COLD) f = pw_pow2_lds(x);
-#endif
+    if (__builtin_expect(!pw_pow2_fast(x, &f), 0)) f = pw_pow2_lds(x);
     return f;
 }
 
@@ -689,12 +652,6 @@ __device__ __forceinline__ void env_forces(const KParams &kp, float mf, float ym
     }
 }
 
-#ifndef WG_FAST_ENV
-#define WG_FAST_ENV 1
-#endif
-#ifndef WG_ENV_PRE
-#define WG_ENV_PRE 1   // barrier-free kernels: the env-force quotients computed before the mass loop (EnvTerms)
-#endif
 // The env forces' quotients of one mass that do not depend on ground contact (gravity, damping), which depend on m and
 // v only: the barrier-free kernels compute them before the mass loop, so after it only their ordered additions and the
 // contact terms remain (env_apply: env_forces<true>'s additions in the same order, bit-identical).  (All nine quotients
@@ -740,27 +697,24 @@ __device__ __forceinline__ void mass_tail(const KParams &kp, float mf, float ymf
     px = p3[0]; py = p3[1]; pz = p3[2];
     if (WG_ABLATE & 256) {   // (ablation: no env forces)
         hit = py < kp.ground;
-    } else if (WG_FAST_ENV && pre) {
+    } else if (pre) {
         // the contact-free quotients came from env_terms before the mass loop
         const float sx = ax, sy = ay, sz = az;
         int emin = 0;
         env_apply(*pre, kp, mf, ymf, vx, vy, vz, py, ax, ay, az, hit, emin);
-        if (__builtin_expect(!__builtin_isfinite(ax + ay + az) || ((WG_GUARDS & 4) && (emin < TINY_EXP || !divisor_ok(mf))), 0)) {
-            ax = sx; ay = sy; az = sz;
-            env_forces<false>(kp, mf, ymf, vx, vy, vz, py, ax, ay, az, hit, emin);
-        }
-    } else if (WG_FAST_ENV) {
-        const float sx = ax, sy = ay, sz = az;
-        int emin = 0;
-        env_forces<true>(kp, mf, ymf, vx, vy, vz, py, ax, ay, az, hit, emin);
-        // cold: redo with exact quotients (a non-finite sum, a dividend or the mass outside the exact range)
-        if (__builtin_expect(!__builtin_isfinite(ax + ay + az) || ((WG_GUARDS & 4) && (emin < TINY_EXP || !divisor_ok(mf))), 0)) {
+        if (__builtin_expect(!__builtin_isfinite(ax + ay + az) || emin < TINY_EXP || !divisor_ok(mf), 0)) {
             ax = sx; ay = sy; az = sz;
             env_forces<false>(kp, mf, ymf, vx, vy, vz, py, ax, ay, az, hit, emin);
         }
     } else {
+        const float sx = ax, sy = ay, sz = az;
         int emin = 0;
-        env_forces<false>(kp, mf, ymf, vx, vy, vz, py, ax, ay, az, hit, emin);
+        env_forces<true>(kp, mf, ymf, vx, vy, vz, py, ax, ay, az, hit, emin);
+        // cold: redo with exact quotients (a non-finite sum, a dividend or the mass outside the exact range)
+        if (__builtin_expect(!__builtin_isfinite(ax + ay + az) || emin < TINY_EXP || !divisor_ok(mf), 0)) {
+            ax = sx; ay = sy; az = sz;
+            env_forces<false>(kp, mf, ymf, vx, vy, vz, py, ax, ay, az, hit, emin);
+        }
     }
     if (pinned) { ax = 0.f; ay = 0.f; az = 0.f; }   // DingPoint.forced is a no-op: a stays zeros()
     // v += a*t in both integrators; the position update differs (a wave-uniform branch on the parameter, on
@@ -865,9 +819,6 @@ __device__ __forceinline__ void mass_accumulate(const TS &ts, const uint16_t *in
 // clamp on the read-ahead: the entries after a mass's list are the next mass's, and the tile's last list is
 // followed by a zero word (the wave writes one after its incidence words), so every read-ahead is a valid entry
 // whose values go unused.  Arithmetic and its order are those of acc_f64_entry<true> (bit-identical).
-#ifndef WG_MASS_V2
-#define WG_MASS_V2 1
-#endif
 __device__ __forceinline__ IncTerm inc_term_at(const char *tb, const char *fb, uint32_t ent) {
     const uint32_t e = ent >> 1;
     const double *t = reinterpret_cast<const double *>(tb + __umul24(e, 24u));
@@ -917,7 +868,7 @@ __device__ __forceinline__ void mass_accumulate_v2(const TermsAoS &ts, const uin
     }
     // a non-finite sum (some quotient was not exact, or an input not finite), a damping force of the wave outside the
     // float32 quotient's exact range (force), or a mass outside its divisor range: redo the list with IEEE divisions
-    if (__builtin_expect(force || ((WG_GUARDS & 8) && !divisor_ok(mf)) ||
+    if (__builtin_expect(force || !divisor_ok(mf) ||
                          !(__builtin_isfinite(ax) && __builtin_isfinite(ay) && __builtin_isfinite(az)), 0)) {
         ax = 0.f; ay = 0.f; az = 0.f;
         for (int r = s0; r < s1; r++) {
@@ -1017,16 +968,13 @@ __device__ inline float seq_sum_quad(float x) {
     a = a + quad_bcast<2>(x);
     return a + quad_bcast<3>(x);
 }
-#ifndef WG_SEQ3
-#define WG_SEQ3 1
-#endif
 __device__ inline void seq_sum3_lanes(float x, float y, float z, int base, int M, float &sx, float &sy, float &sz) {
     float a, b, c;
     if (M == 4) {
         sx = seq_sum_quad(x); sy = seq_sum_quad(y); sz = seq_sum_quad(z);
         return;
     }
-    if (WG_SEQ3 && M == 16) {
+    if (M == 16) {
         // the three chains interleaved in one unrolled body (three independent DPP adds per step instead of one chain
         // at a time behind a scalar loop); the empty asm keeps each chain's adds scalar (no SLP packing, which has
         // no DPP form)
@@ -1076,15 +1024,12 @@ __device__ inline float pw_sum_lanes(float x, int base, int M, int lane) {
 // M = 4 and M = 16 (Balance-v0 / Box-v0 and the canonical walker) the seven chains run interleaved in one
 // straight-line block — every DPP add has six independent ones to fill its wait states, where the generic path
 // (M known only at run time) runs each sum behind its own branches — with the same additions in the same order.
-#ifndef WG_SUMS7
-#define WG_SUMS7 1
-#endif
 struct WalkerSums { float sx, sy, sz, ysum, vsum, ksum, psum; };
 #define WG_OPAQUE7(a, b, c, d, e, f, g) asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e), "+v"(f), "+v"(g))
 __device__ inline WalkerSums walker_sums(float px, float py, float pz, float nv, float ke, float pe, int base, int M,
                                          int lane) {
     WalkerSums r;
-    if (WG_SUMS7 && M == 4) {
+    if (M == 4) {
         // a walker is one DPP quad: every lane adds the quad's four values in order (M < 8: pairwise == sequential)
         // (x_0 + 0 with the zero in a register: one v_add_f32_dpp each, no separate DPP move; x + 0 == 0 + x)
         float z = 0.f;
@@ -1109,7 +1054,7 @@ __device__ inline WalkerSums walker_sums(float px, float py, float pz, float nv,
         r.sx = a; r.sy = b; r.sz = c; r.ysum = b; r.vsum = d; r.ksum = e; r.psum = f;
         return r;
     }
-    if (WG_SUMS7 && M == 16) {
+    if (M == 16) {
         // sequential: s_q <- s_{q-1} + x_q along the row (lane base + 15 ends with the walker's left-to-right sum);
         // pairwise: r_j = x_j + x_{j+8}, then ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) by quad_perm / half-mirror moves
         float a = 0.f + px, b = 0.f + py, c = 0.f + pz;
@@ -1142,9 +1087,6 @@ __device__ inline WalkerSums walker_sums(float px, float py, float pz, float nv,
 #undef WG_OPAQUE7
 
 // ------------------------------------------------------------------ pair terms
-#ifndef WG_FAST_PAIR
-#define WG_FAST_PAIR 1   // 0 (A/B builds only): every pair term in its IEEE form
-#endif
 // One gravity / coulomb partner (gym/engine.py:128-147 -> anti_forced :69-76 -> forced :65-67), all float64:
 // r = max(norm(d) as float64, Config.r); f = -c*s_lo*s_hi / r**2; a = f32(f64(a) + ((-f)*d / r) / m).  The
 // divisions by r (when unclamped: a float32 value) and by m go through ddiv_f32d with one IEEE reciprocal each.
@@ -1270,8 +1212,8 @@ template <bool LDS_TAB = false>
 __device__ __forceinline__ void g2_gravity_term(double cgd, float d0, float d1, float d2, float mf, double ym,
                                                 float &ax, float &ay, float &az) {
     float q0, q1, q2;
-    bool ok = WG_FAST_PAIR;
-    if (WG_FAST_PAIR) g2_gravity_fast<LDS_TAB>((float)cgd, d0, d1, d2, ym, q0, q1, q2, ok);
+    bool ok;
+    g2_gravity_fast<LDS_TAB>((float)cgd, d0, d1, d2, ym, q0, q1, q2, ok);
     if (__builtin_expect(!ok || !divisor_ok(mf), 0)) g2_gravity_cold(cgd, d0, d1, d2, mf, q0, q1, q2);
     ax = ax + q0;
     ay = ay + q1;
@@ -1291,8 +1233,8 @@ __device__ void pair_electrostatic_lds(const wg_batch &b, const KParams &kp, con
     const float *p3 = spos + 3 * (lm + q);
     const double sq = b.charge ? b.charge[g0 + q] : kp.pair_e;
     const float sx = ax, sy = ay, sz = az;
-    bool bad = !WG_FAST_PAIR;
-    if (WG_FAST_PAIR) {
+    bool bad = false;
+    {
         for (int pj = 0; pj < M; pj++) {
             if (pj == q) continue;
             const float *o3 = spos + 3 * (lm + pj);
@@ -1324,8 +1266,8 @@ __device__ __forceinline__ void pair_central_pass_lds(const wg_batch &b, double 
         return GRAV ? (double)sm[lm + pj] : (b.charge ? (double)b.charge[g0 + pj] : pe);
     };
     const float sx = ax, sy = ay, sz = az;
-    bool bad = !WG_FAST_PAIR;
-    if (WG_FAST_PAIR && M > 0) {
+    bool bad = false;
+    if (M > 0) {
         const float *o3 = spos + 3 * lm;
         float n0 = o3[0], n1 = o3[1], n2 = o3[2];
         double ns = strength(0);
@@ -1404,11 +1346,8 @@ __device__ void pair_forces_lds(const wg_batch &b, const KParams &kp, const floa
 // is 5 waves per SIMD, which a 512-thread workgroup rounds down to 4): 4,096 chains of 100 masses 159.6 -> 153.8 us
 // per launch, the performance_demo loop 181.9 -> 173.4 (profiles/r03v_ab_wg_occupancy.json); 7 spills more and
 // gains less.  The PWD 3 and shuffle instances would spill 48-116 B at 80 VGPRs and keep the compiler's choice.
-#ifndef WG_WG_OCC
-#define WG_WG_OCC 6
-#endif
 template <bool STEP, bool RAGGED, bool IN3D, int PWD, bool SHFL>
-constexpr int wg_kernel_waves() { return (STEP && PWD == 0 && !SHFL && WG_WG_OCC) ? WG_WG_OCC : 1; }
+constexpr int wg_kernel_waves() { return (STEP && PWD == 0 && !SHFL) ? 6 : 1; }
 template <bool STEP, bool RAGGED, bool IN3D, int PWD, bool SHFL>
 __global__ __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(wg_kernel_waves<STEP, RAGGED, IN3D, PWD, SHFL>()))) void walker_step_kernel(
     wg_batch b, KParams kp, const float *__restrict__ action, int action_cols, int action_stride,
@@ -1520,7 +1459,7 @@ __global__ __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(wg_kernel_
         }
         s.x[u] = x;
     }
-    if (WG_SQ_LDS) pw_tables_to_lds(tid);   // (np_sq_t's cold path: the pair passes, the energy terms)
+    pw_tables_to_lds(tid);   // (np_sq_t's cold path: the pair passes, the energy terms)
     __syncthreads();
 
     // registers of this lane's (first) mass after the physics: feed the SHFL reductions and obs
@@ -1856,15 +1795,6 @@ __device__ __forceinline__ float lane_gather(float v, int src_byte) {
     return __int_as_float(__builtin_amdgcn_ds_bpermute(src_byte, __float_as_int(v)));
 }
 
-#ifndef WG_FAST_SPRING
-#define WG_FAST_SPRING 1
-#endif
-#ifndef WG_QMOVE
-#define WG_QMOVE 0   // A/B builds only: the lean kernel's quotients t/m and df/m formed once per
-#endif               // spring end in the edge phase (72 B of LDS per spring) instead of once per incidence entry
-#ifndef WG_SPRING_CHK
-#define WG_SPRING_CHK 1   // the fast spring path's range test on nf instead of finiteness tests of every quotient
-#endif
 // Spring term and damping force of one edge from its endpoints' state (gathered from the mass lanes):
 // spring_edge's arithmetic with the cheaper reciprocal (identical results; cold path unchanged).
 // Cold path: every quantity again with IEEE divisions and numpy's sqrt (exact for every input).
@@ -1896,7 +1826,6 @@ __device__ __forceinline__ void spring_terms(const EdgeRec &e, float x, float pi
                                              float &g1, float &g2, int spring_mode, bool pos_ok) {
     const float r0 = pjx - pix, r1 = pjy - piy, r2 = pjz - piz;     // other.pos - self.pos
     float d0, d1, d2;
-#if WG_FAST_SPRING
     // np.linalg.norm(p_i - p_j) (engine.py:86): squares summed in float64, rounded, sqrt.  (p_i - p_j)^2 == r^2.
     const float sq = (float)(((double)(r0 * r0) + (double)(r1 * r1)) + (double)(r2 * r2));
     // sqrt_mid's range is [2^-96, 2^126); the d quotients' exact range asks cur in [2^-20, 2^20) (false for NaN)
@@ -1918,22 +1847,13 @@ __device__ __forceinline__ void spring_terms(const EdgeRec &e, float x, float pi
         t2 = ddiv_fast((double)(nf * r2), dist, yc);
     }
     bool rok = true;
-    if ((WG_GUARDS & 1) && __builtin_expect(!pos_ok, 0)) rok = fexp3(r0, r1, r2) >= TINY_EXP;
-#if WG_SPRING_CHK
+    if (__builtin_expect(!pos_ok, 0)) rok = fexp3(r0, r1, r2) >= TINY_EXP;
     // mid holds only for finite differences with |r| < 2^20 (an inf / NaN / overflowing square fails it), so the d
     // quotients are finite; |nf| < 2^100 (false for NaN) keeps nf * r below 2^120 and every t quotient finite and in
     // Markstein's exact range (|t| in [2^-170, 2^140] or 0): the same lanes' quotients as the finiteness tests of
     // d and t certified, with five fewer VALU (a larger |nf| now takes the exact cold path too: same results)
     const bool fast_ok = mid && rok && __builtin_fabsf(nf) < 0x1p100f;
-#else
-    // the quotients are exact when every one is finite; a non-finite one makes its sum non-finite (|d| <= 1
-    // cannot overflow a sum of three)
-    const bool fast_ok = mid && rok && __builtin_isfinite(d0 + d1 + d2) && __builtin_isfinite(t0 + t1 + t2);
-#endif
     if (__builtin_expect(!fast_ok, 0)) spring_terms_cold(e, x, r0, r1, r2, t0, t1, t2, d0, d1, d2, spring_mode);
-#else
-    spring_terms_cold(e, x, r0, r1, r2, t0, t1, t2, d0, d1, d2, spring_mode);
-#endif
     const float dk = np_dot3(vix - vjx, viy - vjy, viz - vjz, d0, d1, d2);  // optimized_walker.py:102-103
     const float dkc = dk * e.c;                                               // :104
     g0 = dkc * d0; g1 = dkc * d1; g2 = dkc * d2;
@@ -1950,7 +1870,7 @@ __device__ __forceinline__ void spring_edge_regs(const EdgeRec &e, int le, float
     spring_terms(e, x, pix, piy, piz, pjx, pjy, pjz, vix, viy, viz, vjx, vjy, vjz, t0, t1, t2, g0, g1, g2, spring_mode,
                  pos_ok);
     ts.put(le, t0, t1, t2, g0, g1, g2);
-    if (WG_GUARDS & 2) gt = gt || fexp3(g0, g1, g2) < TINY_EXP;
+    gt = gt || fexp3(g0, g1, g2) < TINY_EXP;
 }
 
 // ------------------------------------------------------------------ lean wave tile: loads, then compute
@@ -1993,127 +1913,75 @@ __device__ __forceinline__ LeanTile lean_tile_of(const wg_batch &b, const float 
 // words, mass-loop inputs, muscles.  (Issuing what the springs need first and the mass-loop inputs last measured
 // 48.5 against 47.7 us per launch, profiles/r02_ab_loadorder_karg.json: in steady state a wave spends ~4K of its
 // ~25K cycles on loads, so there is little latency left to hide.)
-#ifndef WG_LEAN_CLAMP
-#define WG_LEAN_CLAMP 1
-#endif
 // A global array element at a 32-bit byte offset from a kernel-argument base: the address is SGPR base + zero-extended
 // VGPR offset, which the global_load's saddr form takes as is (no 64-bit address arithmetic per load).
 template <typename T>
 __device__ __forceinline__ const T &at_u32(const T *base, uint32_t byte_off) {
-    // (WG_LEAN_CLAMP=0, A/B builds only: a sign-extended offset, which keeps the 64-bit VALU address arithmetic)
-    const size_t off = WG_LEAN_CLAMP ? (size_t)byte_off : (size_t)(int64_t)(int32_t)byte_off;
-    return *reinterpret_cast<const T *>(reinterpret_cast<const char *>(base) + off);
+    return *reinterpret_cast<const T *>(reinterpret_cast<const char *>(base) + (size_t)byte_off);
 }
 // The same form for the stores (global_store's saddr form): the lean and wave kernels' outputs, whose byte offsets the
-// host bounds below 4 GiB (u32_bytes, obs_u32).  WG_ST_U32=0 (A/B builds only) keeps the 64-bit element addressing.
-#ifndef WG_ST_U32
-#define WG_ST_U32 1
-#endif
+// host bounds below 4 GiB (u32_bytes, obs_u32).
 template <typename T>
 __device__ __forceinline__ T &at_u32w(T *base, uint32_t byte_off) {
     return *reinterpret_cast<T *>(reinterpret_cast<char *>(base) + (size_t)byte_off);
 }
-// a walker's (or mass's) element e of a record of n floats: 64-bit element arithmetic, or the 32-bit byte offset
-#define WG_ST(base, e, n) (WG_ST_U32 ? &at_u32w((base), (uint32_t)(n) * 4u * (uint32_t)(e)) : (base) + (size_t)(n) * (size_t)(e))
+// a walker's (or mass's) element e of a record of n floats, as a 32-bit byte offset
+#define WG_ST(base, e, n) (&at_u32w((base), (uint32_t)(n) * 4u * (uint32_t)(e)))
 // a count (<= 64) halved and negated as the reference's float64 product: exact in float32 (-0.0 for 0, as -(0.0) * 0.5)
 __device__ __forceinline__ float neg_half_count(int n) { return -0.5f * (float)n; }
 template <int NE>
 __device__ __forceinline__ void lean_load_mass(const wg_batch &b, const LeanTile &t, int lane, LeanIn<NE> &L) {
     L.mf = 0.f; L.io0 = 0; L.io1 = 0; L.wsteps = 0; L.pin = 0;
-    if (WG_LEAN_CLAMP) {
-        // every lane loads (lanes past the tile's masses a duplicate of its last one; their values are never used)
-        const int ln = min(lane, t.nP - 1);
-        const int wl = ln >> (31 - __builtin_clz(b.M)), q = ln & (b.M - 1);
-        L.mf = at_u32(b.mass, 4u * (t.P0 + ln));
-        if (b.pinned) L.pin = at_u32(b.pinned, t.P0 + ln);
-        const uint32_t io = (uint32_t)(t.w0 + wl) * (b.M + 1) + q;
-        L.io0 = at_u32(b.inc_off, 2u * io); L.io1 = at_u32(b.inc_off, 2u * io + 2u);
-        L.wsteps = at_u32(b.steps, 4u * (uint32_t)(t.w0 + wl));   // the walker's counter in each of its lanes
-        return;
-    }
-    const uint32_t pl = t.P0 + lane;
-    if (t.is_mass) {
-        L.mf = b.mass[pl];
-        if (b.pinned) L.pin = b.pinned[pl];
-        const uint32_t io = (uint32_t)(t.w0 + t.wl) * (b.M + 1) + t.q;
-        L.io0 = b.inc_off[io]; L.io1 = b.inc_off[io + 1];
-        if (t.q == 0) L.wsteps = b.steps[(uint32_t)(t.w0 + t.wl)];
-    }
+    // every lane loads (lanes past the tile's masses a duplicate of its last one; their values are never used)
+    const int ln = min(lane, t.nP - 1);
+    const int wl = ln >> (31 - __builtin_clz(b.M)), q = ln & (b.M - 1);
+    L.mf = at_u32(b.mass, 4u * (t.P0 + ln));
+    if (b.pinned) L.pin = at_u32(b.pinned, t.P0 + ln);
+    const uint32_t io = (uint32_t)(t.w0 + wl) * (b.M + 1) + q;
+    L.io0 = at_u32(b.inc_off, 2u * io); L.io1 = at_u32(b.inc_off, 2u * io + 2u);
+    L.wsteps = at_u32(b.steps, 4u * (uint32_t)(t.w0 + wl));   // the walker's counter in each of its lanes
 }
 template <int NE>
 __device__ __forceinline__ void lean_load_muscles(const wg_batch &b, const KParams &kp, const float *__restrict__ action,
                                                   int action_stride, const LeanTile &t, int lane, LeanIn<NE> &L) {
     L.x = 0.f; L.lo = 0.f; L.hi = 0.f; L.stp = 0.f; L.a = 0.f;
-    if (WG_LEAN_CLAMP) {
-        if (t.nU > 0) {                       // wave-uniform
-            const uint32_t ul = t.U0 + min(lane, t.nU - 1);
-            L.x = at_u32(b.muscle_x, 4u * ul);
-            if (action && action_stride > 0) {
-                const float2 bd = at_u32(reinterpret_cast<const float2 *>(b.muscle_bounds), 8u * ul);
-                L.lo = bd.x; L.hi = bd.y;
-                if (kp.action_mode == 1) L.stp = at_u32(b.muscle_stride, 4u * ul);
-                const int wl = min(t.mu_wl, t.nw - 1), ua = max(0, min(t.mu_ua, action_stride - 1));
-                L.a = at_u32(action, 4u * ((uint32_t)(t.w0 + wl) * (uint32_t)action_stride + (uint32_t)ua));
-            }
-        }
-        return;
-    }
-    const uint32_t ul = t.U0 + lane;        // this lane's muscle
-    if (t.is_mus) {
-        L.x = b.muscle_x[ul];
-        if (t.acts) {
-            const float2 bd = reinterpret_cast<const float2 *>(b.muscle_bounds)[ul];
+    if (t.nU > 0) {                       // wave-uniform
+        const uint32_t ul = t.U0 + min(lane, t.nU - 1);
+        L.x = at_u32(b.muscle_x, 4u * ul);
+        if (action && action_stride > 0) {
+            const float2 bd = at_u32(reinterpret_cast<const float2 *>(b.muscle_bounds), 8u * ul);
             L.lo = bd.x; L.hi = bd.y;
-            if (kp.action_mode == 1) L.stp = b.muscle_stride[ul];
-            L.a = action[(uint32_t)(t.w0 + t.mu_wl) * (uint32_t)action_stride + (uint32_t)t.mu_ua];
+            if (kp.action_mode == 1) L.stp = at_u32(b.muscle_stride, 4u * ul);
+            const int wl = min(t.mu_wl, t.nw - 1), ua = max(0, min(t.mu_ua, action_stride - 1));
+            L.a = at_u32(action, 4u * ((uint32_t)(t.w0 + wl) * (uint32_t)action_stride + (uint32_t)ua));
         }
     }
 }
 template <int NE>
 __device__ __forceinline__ void lean_load(const wg_batch &b, const KParams &kp, const float *__restrict__ action,
                                           int action_stride, const LeanTile &t, int lane, LeanIn<NE> &L) {
-    if (WG_LEAN_CLAMP) {
-        // every load unconditional from a clamped (valid) index, issued back to back: no exec-mask branch per load
-        // (each with its zero-fill moves), addresses as SGPR base + 32-bit offset.  Lanes past the tile's masses,
-        // springs and muscles hold duplicates; every use of them is gated (is_mass, le < nE, is_mus, acts).
-        const uint32_t pl = t.P0 + min(lane, t.nP - 1);
-        const float *gp = &at_u32(b.pos, 12u * pl), *gv = &at_u32(b.vel, 12u * pl);
-        L.p3[0] = gp[0]; L.p3[1] = gp[1]; L.p3[2] = gp[2];
-        L.v3[0] = gv[0]; L.v3[1] = gv[1]; L.v3[2] = gv[2];
-#pragma unroll
-        for (int it = 0; it < NE; it++) {
-            const uint32_t le = t.E0 + (uint32_t)min(lane + 64 * it, t.nE - 1);
-            const uint4 v = at_u32(reinterpret_cast<const uint4 *>(b.edges), 16u * le);
-            L.er[it] = EdgeRec{v.x, __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w)};
-            L.gi[it] = at_u32(reinterpret_cast<const uint32_t *>(b.inc), 4u * le);
-        }
-        lean_load_mass<NE>(b, t, lane, L);
-        lean_load_muscles<NE>(b, kp, action, action_stride, t, lane, L);
-        if (!t.is_mass) {                     // the reference values of the lanes past the tile's masses
-            L.p3[0] = 0.f; L.p3[1] = 0.f; L.p3[2] = 0.f; L.v3[0] = 0.f; L.v3[1] = 0.f; L.v3[2] = 0.f;
-            L.mf = 0.f; L.pin = 0; L.io0 = 0; L.io1 = 0;
-        }
-        if (!t.is_mus) { L.x = 0.f; L.lo = 0.f; L.hi = 0.f; L.stp = 0.f; }
-        if (!t.acts) L.a = 0.f;
-        return;
-    }
-    const uint32_t pl = t.P0 + lane;        // this lane's mass
-    L.p3[0] = 0.f; L.p3[1] = 0.f; L.p3[2] = 0.f;
-    L.v3[0] = 0.f; L.v3[1] = 0.f; L.v3[2] = 0.f;
-    if (t.is_mass) {
-        const float *gp = b.pos + 3 * (size_t)pl, *gv = b.vel + 3 * (size_t)pl;
-        L.p3[0] = gp[0]; L.p3[1] = gp[1]; L.p3[2] = gp[2];
-        L.v3[0] = gv[0]; L.v3[1] = gv[1]; L.v3[2] = gv[2];
-    }
-    const uint32_t *incw = reinterpret_cast<const uint32_t *>(b.inc) + t.E0;   // 2 u16 entries per word
+    // every load unconditional from a clamped (valid) index, issued back to back: no exec-mask branch per load
+    // (each with its zero-fill moves), addresses as SGPR base + 32-bit offset.  Lanes past the tile's masses,
+    // springs and muscles hold duplicates; every use of them is gated (is_mass, le < nE, is_mus, acts).
+    const uint32_t pl = t.P0 + min(lane, t.nP - 1);
+    const float *gp = &at_u32(b.pos, 12u * pl), *gv = &at_u32(b.vel, 12u * pl);
+    L.p3[0] = gp[0]; L.p3[1] = gp[1]; L.p3[2] = gp[2];
+    L.v3[0] = gv[0]; L.v3[1] = gv[1]; L.v3[2] = gv[2];
 #pragma unroll
     for (int it = 0; it < NE; it++) {
-        const int le = lane + 64 * it;
-        if (le < t.nE) L.er[it] = load_edge(b.edges, t.E0 + (uint32_t)le);
-        if (le < t.nE) L.gi[it] = incw[(uint32_t)le];
+        const uint32_t le = t.E0 + (uint32_t)min(lane + 64 * it, t.nE - 1);
+        const uint4 v = at_u32(reinterpret_cast<const uint4 *>(b.edges), 16u * le);
+        L.er[it] = EdgeRec{v.x, __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w)};
+        L.gi[it] = at_u32(reinterpret_cast<const uint32_t *>(b.inc), 4u * le);
     }
     lean_load_mass<NE>(b, t, lane, L);
     lean_load_muscles<NE>(b, kp, action, action_stride, t, lane, L);
+    if (!t.is_mass) {                     // the reference values of the lanes past the tile's masses
+        L.p3[0] = 0.f; L.p3[1] = 0.f; L.p3[2] = 0.f; L.v3[0] = 0.f; L.v3[1] = 0.f; L.v3[2] = 0.f;
+        L.mf = 0.f; L.pin = 0; L.io0 = 0; L.io1 = 0;
+    }
+    if (!t.is_mus) { L.x = 0.f; L.lo = 0.f; L.hi = 0.f; L.stp = 0.f; }
+    if (!t.acts) L.a = 0.f;
 }
 
 // double gathered from another lane (two ds_bpermute), all lanes taking part
@@ -2129,9 +1997,6 @@ __device__ __forceinline__ double lane_gather_d(double v, int src_byte) {
 // GPU against pw_pow2 for every float32 bit pattern (scripts/check_pow2_lanes.hip, profiles/r04x_check_pow2_lanes.json);
 // Balance-4096 5.48 -> 5.37 us (the cold path, ~9 % of its waves, cost 0.28 us: RN(x*x) everywhere ran 5.20;
 // profiles/r04x_ab_balance_sq.json).
-#ifndef WG_SQ_REG
-#define WG_SQ_REG 1
-#endif
 __device__ __forceinline__ float pw_pow2_lanes(float x, double tl, double te) {
     unsigned int ix = pw_asu32(x) & 0x7fffffffu;
     const bool special = ix == 0u || ix >= 0x7f800000u;          // zero, inf, nan: glibc returns x * x
@@ -2198,8 +2063,8 @@ __device__ __forceinline__ void pair_central(double coef, double sq, const float
     const int gb = lane & ~(M - 1), q = lane & (M - 1);
     const double md = (double)mf, ym = 1.0 / md;
     const float sx = ax, sy = ay, sz = az;
-    bool bad = !WG_FAST_PAIR && is_mass;
-    if (WG_FAST_PAIR) {
+    bool bad = false;
+    {
         for (int pj = 0; pj < M; pj++) {
             const int src = (gb + pj) << 2;
             const float ox = lane_gather(p3[0], src), oy = lane_gather(p3[1], src), oz = lane_gather(p3[2], src);
@@ -2327,9 +2192,9 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
     float *s_x = reinterpret_cast<float *>(sl + lg.off_x);
     const float mf = L.mf;
     const bool pin = L.pin != 0;
-    // (WG_SQ_REG, NE = 1: glibc's powf tables in registers, lane l < 32 holding entry l of each)
+    // (NE = 1: glibc's powf tables in registers, lane l < 32 holding entry l of each)
     double sq_tl = 0.0, sq_te = 0.0;
-    if (WG_SQ_REG && NE == 1 && !RES) {   // (not the resident kernel: its carried state holds the registers)
+    if (NE == 1 && !RES) {   // (not the resident kernel: its carried state holds the registers)
         sq_tl = PW_LOG2_TAB[lane & 31];
         sq_te = pw_asdouble(PW_EXP2_TAB[lane & 31]);
     }
@@ -2339,7 +2204,7 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
 #pragma unroll
         for (int it = 0; it < NE; it++)
             if (lane + 64 * it < nE) s_inc[lane + 64 * it] = L.gi[it];
-        if (WG_MASS_V2 && lane == 0) s_inc[nE] = 0u;   // the read-ahead pad after the last list (mass_accumulate_v2)
+        if (lane == 0) s_inc[nE] = 0u;   // the read-ahead pad after the last list (mass_accumulate_v2)
     }
     float x = L.x;
     if (acts) {
@@ -2351,7 +2216,7 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
     if (is_mus) s_x[lane] = x;
     double ym = recip_m(mf);        // RN64(1/m) of this lane's mass: every /m below is exact from it
     // (opaque: otherwise the compiler turns (float)ym, which is RN32(1/m), into a second, float32 IEEE division)
-    if (WG_MASS_V2 && !RES) asm volatile("" : "+v"(ym));
+    if (!RES) asm volatile("" : "+v"(ym));
     wave_sync();
     STAMP(2);
 
@@ -2387,53 +2252,13 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
         const bool mus = le < nE && ew < A;
         const float xs = s_x[mus ? (int)__umul24(ewl, A) + ew : 0];
         const float xr = mus ? xs : e.rest;
-#if WG_QMOVE
-        // both ends' masses and reciprocals from the mass lanes (every lane takes part in the gathers)
-        const int ewl2 = fdiv(le, K, lg.invK);
-        const int qbi = (ewl2 * M + edge_i(e.ij)) << 2, qbj = (ewl2 * M + edge_j(e.ij)) << 2;
-        const float mi = lane_gather(mf, qbi), mj = lane_gather(mf, qbj);
-        const double ymi = lane_gather_d(ym, qbi), ymj = lane_gather_d(ym, qbj);
-#endif
         if (le < nE) {
             if (WG_ABLATE & 1) {   // profiling builds only: no spring arithmetic
                 ts.put(le, xr + g.v[0] + g.v[3] + g.v[6] + g.v[9], g.v[1] + g.v[4] + g.v[7] + g.v[10],
                        g.v[2] + g.v[5] + g.v[8] + g.v[11], e.k, e.c, 0.f);
             } else {
-#if WG_QMOVE
-              if (RES) {   // (the resident kernel is not part of the A/B: it keeps the per-entry quotients)
-                spring_edge_regs(e, le, xr, g.v[0], g.v[1], g.v[2], g.v[3], g.v[4], g.v[5], g.v[6], g.v[7], g.v[8],
-                                 g.v[9], g.v[10], g.v[11], ts, 0, gtiny, pos_ok);
-              } else {
-                double t0, t1, t2;
-                float g0, g1, g2;
-                spring_terms(e, xr, g.v[0], g.v[1], g.v[2], g.v[3], g.v[4], g.v[5], g.v[6], g.v[7], g.v[8], g.v[9],
-                             g.v[10], g.v[11], t0, t1, t2, g0, g1, g2, 0, pos_ok);
-                const double mdi = (double)mi, mdj = (double)mj;
-                const float ymfi = (float)ymi, ymfj = (float)ymj;
-                double qi0 = ddiv_fast(t0, mdi, ymi), qi1 = ddiv_fast(t1, mdi, ymi), qi2 = ddiv_fast(t2, mdi, ymi);
-                double qj0 = ddiv_fast(t0, mdj, ymj), qj1 = ddiv_fast(t1, mdj, ymj), qj2 = ddiv_fast(t2, mdj, ymj);
-                float di0 = fdiv_fast(g0, mi, ymfi), di1 = fdiv_fast(g1, mi, ymfi), di2 = fdiv_fast(g2, mi, ymfi);
-                float dj0 = fdiv_fast(g0, mj, ymfj), dj1 = fdiv_fast(g1, mj, ymfj), dj2 = fdiv_fast(g2, mj, ymfj);
-                // the mass loop's guards, per spring: a damping force below the f32 quotient's exact range, a mass
-                // outside its divisor range, or a non-finite quotient: this spring's quotients as IEEE divisions
-                const bool bad = fexp3(g0, g1, g2) < TINY_EXP || !divisor_ok(mi) || !divisor_ok(mj) ||
-                                 !__builtin_isfinite(((qi0 + qi1) + (qi2 + qj0)) + (qj1 + qj2)) ||
-                                 !__builtin_isfinite(((di0 + di1) + (di2 + dj0)) + (dj1 + dj2));
-                if (__builtin_expect(bad, 0)) {
-                    qi0 = t0 / mdi; qi1 = t1 / mdi; qi2 = t2 / mdi; qj0 = t0 / mdj; qj1 = t1 / mdj; qj2 = t2 / mdj;
-                    di0 = g0 / mi; di1 = g1 / mi; di2 = g2 / mi; dj0 = g0 / mj; dj1 = g1 / mj; dj2 = g2 / mj;
-                }
-                // record of spring le: [+t/m_i x3 | -t/m_j x3] f64, then [-df/m_i x3 | +df/m_j x3] f32: end i adds
-                // +t/m_i then -df/m_i, end j -t/m_j then +df/m_j (acc_entry_v2's signs, exact negations)
-                double *qr = reinterpret_cast<double *>(sl) + 9 * le;
-                qr[0] = qi0; qr[1] = qi1; qr[2] = qi2; qr[3] = -qj0; qr[4] = -qj1; qr[5] = -qj2;
-                float *dr = reinterpret_cast<float *>(qr + 6);
-                dr[0] = -di0; dr[1] = -di1; dr[2] = -di2; dr[3] = dj0; dr[4] = dj1; dr[5] = dj2;
-              }
-#else
                 spring_edge_regs(e, le, xr, g.v[0], g.v[1], g.v[2], g.v[3], g.v[4], g.v[5], g.v[6], g.v[7], g.v[8],
                                  g.v[9], g.v[10], g.v[11], ts, 0, gtiny, pos_ok);   // lean path: spring_mode 0 only
-#endif
             }
         }
     };
@@ -2457,7 +2282,7 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
     // registers are free: after the loop only their ordered additions remain (the resident kernel, whose state
     // registers are tight, keeps them in mass_tail)
     EnvTerms et{};
-    if (WG_ENV_PRE && !RES) et = env_terms(kp, mf, (float)ym, L.v3[0], L.v3[1], L.v3[2]);
+    if (!RES) et = env_terms(kp, mf, (float)ym, L.v3[0], L.v3[1], L.v3[2]);
     float px = 0.f, py = 0.f, pz = 0.f, vx = 0.f, vy = 0.f, vz = 0.f, ax = 0.f, ay = 0.f, az = 0.f;
     float nv = 0.f, ke = 0.f, pe = 0.f;
     bool hit = false;
@@ -2465,19 +2290,7 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
         const int r1 = (WG_ABLATE & 2) ? min(L.io1, L.io0 + 1) : L.io1;
         const int lb = wl * K;
         // (the resident kernel keeps the XOR sign form: 5 fewer registers where its carried state is live)
-        if (WG_QMOVE && !RES) {
-            // quotient records (72 B per spring): end e of spring le at 72 le + 24 e (f64 x3) and 72 le + 48 + 12 e
-            const uint16_t *p = reinterpret_cast<const uint16_t *>(s_inc) + 2 * lb;
-            const char *base = sl + 72 * lb;
-            for (int r = L.io0; r < r1; r++) {
-                const uint32_t ent = p[r];
-                const char *rec = base + __umul24(ent >> 1, 72u);
-                const double *q = reinterpret_cast<const double *>(rec + 24 * (ent & 1u));
-                const float *dq = reinterpret_cast<const float *>(rec + 48 + 12 * (ent & 1u));
-                ax = (float)((double)ax + q[0]); ay = (float)((double)ay + q[1]); az = (float)((double)az + q[2]);
-                ax = ax + dq[0]; ay = ay + dq[1]; az = az + dq[2];
-            }
-        } else if (WG_MASS_V2 && !RES)
+        if (!RES)
             mass_accumulate_v2(ts, reinterpret_cast<const uint16_t *>(s_inc) + 2 * lb, lb, L.io0, r1, mf, ym, ax, ay, az,
                                wave_tiny);
         else
@@ -2488,13 +2301,13 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
     if (!RES && kp.pair_mode) pair_forces(b, kp, L.p3, mf, pl, lane, M, is_mass, ax, ay, az);
     if (is_mass) {
         mass_tail(kp, mf, (float)ym, L.p3, L.v3, px, py, pz, vx, vy, vz, ax, ay, az, hit, pin,
-                  (WG_ENV_PRE && !RES) ? &et : nullptr);
+                  !RES ? &et : nullptr);
         if (b.radius && store) b.radius[pl] = hit ? 3.0 : 1.0;   // p.r = 3 / p.r = 1 (gym/optimized_env.py:156,175)
         nv = np_norm3(vx, vy, vz);
-        if (!(WG_SQ_REG && NE == 1 && !RES)) ke = mf * np_sq<NE == 1>(nv);   // p.m * norm(p.v) ** 2 (gym/optimized_env.py:242)
+        if (!(NE == 1 && !RES)) ke = mf * np_sq<NE == 1>(nv);   // p.m * norm(p.v) ** 2 (gym/optimized_env.py:242)
         pe = (float)((double)mf * kp.g) * (py - kp.ground);
     }
-    if (WG_SQ_REG && NE == 1 && !RES) {   // every lane (table gathers); lanes past the masses square 0
+    if (NE == 1 && !RES) {   // every lane (table gathers); lanes past the masses square 0
         const float sq = np_sq_wave(nv, sq_tl, sq_te);
         if (is_mass) ke = mf * sq;
     }
@@ -2595,12 +2408,7 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
 
 // NE spring passes per wave need up to 8 x 16-B records in registers: 6 waves per SIMD hold up to NE 4 without
 // spills, NE 8 (up to 512 springs per 64 lanes) gets the 4-wave register budget.
-#ifndef WG_NE1_WAVES
-#define WG_NE1_WAVES 6   // A/B builds only: the register budget of the NE = 1 instance (small, latency-bound batches)
-#endif
-constexpr int lean_waves(int NE) {   // (QMOVE: its LDS allows 3 per SIMD)
-    return WG_QMOVE ? 3 : NE >= 8 ? 4 : NE == 1 ? WG_NE1_WAVES : 6;
-}
+constexpr int lean_waves(int NE) { return NE >= 8 ? 4 : 6; }
 
 // One tile (64 / M walkers) per wave; waves never wait for one another.
 template <bool IN3D, int NE>
@@ -2634,11 +2442,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lean_waves(
 // outputs; pos / vel / acc / contact / muscle x / steps go to HBM after the last step.  Same arithmetic as
 // walker_step_lean, step for step (bit-identical to n_steps single-step launches).
 template <bool IN3D, int NE>
-#ifndef WG_RES_WAVES
-#define WG_RES_WAVES 5   // waves per SIMD the resident kernel's register budget targets (its state stays live):
-#endif                   // 5 since the scalar wave index (16 B of scratch at NE 3-4): 35.49 against 36.07 us per step
-                         // at 4 (profiles/r04l_ab_resident.json)
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4 : WG_RES_WAVES))) void walker_rollout_lean(
+// (register budget: 5 waves per SIMD since the scalar wave index, 16 B of scratch at NE 3-4: 35.49 against 36.07 us per
+// step at 4, profiles/r04l_ab_resident.json)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4 : 5))) void walker_rollout_lean(
     wg_batch b, KParams kp, const float *__restrict__ action, int action_cols, int action_stride, int64_t action_step,
     KOut o, int n_steps, LeanGeo lg) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -2833,7 +2639,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
 #pragma unroll
     for (int it = 0; it < NE; it++)
         if (lane + 64 * it < nE) s_inc[lane + 64 * it] = gi[it];
-    if (WG_MASS_V2 && lane == 0) s_inc[nE] = 0u;   // the read-ahead pad after the last list (mass_accumulate_v2)
+    if (lane == 0) s_inc[nE] = 0u;   // the read-ahead pad after the last list (mass_accumulate_v2)
     float x = mx;
     if (acts) {
         x = (kp.action_mode == 1) ? ((act != 0.f) ? x + mst : x - mst) : x + act;
@@ -2843,7 +2649,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
     }
     if (is_mus) s_x[lane] = x;
     double ym = recip_m(mf);
-    if (WG_MASS_V2) asm volatile("" : "+v"(ym));   // (float)ym stays a conversion, not a float32 division
+    asm volatile("" : "+v"(ym));   // (float)ym stays a conversion, not a float32 division
     wave_sync();
     STAMP(2);
 
@@ -2881,18 +2687,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
 
     // ================= masses: ordered accumulation, env forces, Point.run1 =================
     EnvTerms et{};
-    if (WG_ENV_PRE) et = env_terms(kp, mf, (float)ym, v3[0], v3[1], v3[2]);   // (as the lean kernel)
+    et = env_terms(kp, mf, (float)ym, v3[0], v3[1], v3[2]);   // (as the lean kernel)
     float px = 0.f, py = 0.f, pz = 0.f, vx = 0.f, vy = 0.f, vz = 0.f, ax = 0.f, ay = 0.f, az = 0.f;
     bool hit = false;
     if (is_mass) {
-        if (WG_MASS_V2)
-            mass_accumulate_v2(ts, reinterpret_cast<const uint16_t *>(s_inc) + 2 * mlb, mlb, io0,
-                               (WG_ABLATE & 2) ? min(io1, io0 + 1) : io1, mf, ym, ax, ay, az, wave_tiny);
-        else
-            mass_accumulate<TermsAoS, true>(ts, reinterpret_cast<const uint16_t *>(s_inc) + 2 * mlb, mlb, io0, io1, mf,
-                                            ax, ay, az, 0, wave_tiny);
-        mass_tail(kp, mf, (float)ym, p3, v3, px, py, pz, vx, vy, vz, ax, ay, az, hit, pin != 0,
-                  WG_ENV_PRE ? &et : nullptr);
+        mass_accumulate_v2(ts, reinterpret_cast<const uint16_t *>(s_inc) + 2 * mlb, mlb, io0,
+                           (WG_ABLATE & 2) ? min(io1, io0 + 1) : io1, mf, ym, ax, ay, az, wave_tiny);
+        mass_tail(kp, mf, (float)ym, p3, v3, px, py, pz, vx, vy, vz, ax, ay, az, hit, pin != 0, &et);
         const uint32_t pl = (uint32_t)(P0 + lane);
         float *gpo = WG_ST(b.pos, pl, 3), *gvo = WG_ST(b.vel, pl, 3), *gao = WG_ST(b.acc, pl, 3);
         gpo[0] = px; gpo[1] = py; gpo[2] = pz;
@@ -2926,17 +2727,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
         if (r == 7) {
             const unsigned long long wm = (M == 64) ? ~0ull : (((1ull << M) - 1ull) << lm);
             v = __int_as_float((__popcll(hb & wm) << 1) | ((sb & wm) == wm ? 1 : 0));
-        } else if (WG_DUAL_SUM) {
+        } else {
             // every lane runs both sums (one path): lanes 0-2 keep the sequential one, 3-6 the pairwise one
             const float *src = r == 3 ? s_tp + 3 * lm + 1 : r == 5 ? s_tk + lm : r == 6 ? s_te + lm : s_tn + lm;
             float vs, vp;
             dual_sum_lds(s_tp + 3 * lm + (r < 3 ? r : 0), 3, src, r == 3 ? 3 : 1, M, vs, vp);
             v = r < 3 ? vs : vp;
-        } else if (r < 3) {
-            v = seq_sum_lds(0.f, s_tp + 3 * lm + r, M, 3);
-        } else {
-            const float *src = r == 3 ? s_tp + 3 * lm + 1 : r == 4 ? s_tn + lm : r == 5 ? s_tk + lm : s_te + lm;
-            v = np_pairwise<0>(src, M, r == 3 ? 3 : 1);
         }
         s_red[idx] = v;
     }
@@ -3195,8 +2991,8 @@ Geo ragged_geo(const wg_batch *b) {
 template <bool STEP, bool RAGGED, bool IN3D, int PWD, bool SHFL>
 int launch(const wg_batch *b, const KParams &kp, const float *action, int cols, int astride,
            const wg_outputs &o, const int32_t *plan, int blocks, const Geo &g, hipStream_t stream) {
-    // (+ the static 512 B of the powf tables, WG_SQ_LDS)
-    const int lds_static = WG_SQ_LDS ? (int)(sizeof(s_pw_log2) + sizeof(s_pw_exp2)) : 0;
+    // (+ the static 512 B of the powf tables in LDS)
+    const int lds_static = (int)(sizeof(s_pw_log2) + sizeof(s_pw_exp2));
     if (g.lds + lds_static > LDS_LIMIT)
         return fail(WG_ERANGE, "workgroup needs %d B of LDS (> 160 KiB)", g.lds + lds_static);
     hipLaunchKernelGGL((walker_step_kernel<STEP, RAGGED, IN3D, PWD, SHFL>), dim3(blocks), dim3(g.threads), g.lds, stream,
@@ -3271,16 +3067,11 @@ bool lean_geo(const wg_batch *b, int obs_stride, LeanGeo *out, int spring_mode =
     const int ew = g.wpw * b->K;                          // springs of a full wave tile
     g.pl = (ew + 3) & ~3;                                 // spring-term slots: 16-B aligned regions
     // t (f64 x3) | df (f32 x3) | incidence words | x (observation rows go from registers to HBM, no LDS tile)
-#if WG_QMOVE
-    g.off_df = align16(g.pl * 72);                        // (quotient move: both ends' quotient records, no df)
-    g.off_inc = g.off_df;
-#else
     g.off_df = align16(g.pl * 24);
     g.off_inc = g.off_df + align16(g.pl * 12);
-#endif
     g.off_x = g.off_inc + align16(ew * 4 + 4);              // + the zero word after the last list (mass_accumulate_v2)
     g.slice = g.off_x + align16(std::max(1, g.wpw * b->A) * 4);
-    if (4 * g.slice > (WG_QMOVE ? 120 : 80) * 1024) return false;
+    if (4 * g.slice > 80 * 1024) return false;
     g.invK = 1.f / (float)b->K;
     g.invA = 1.f / (float)std::max(1, b->A);
     g.invM = 1.f / (float)M;
@@ -3480,19 +3271,21 @@ int run(const wg_batch *b, const wg_params *p, const float *action, int32_t cols
     return 0;
 }
 
-// wg_run_ranges' phase skew (WG_RANGE_SKEW_US): one wave that waits `ticks` of the 100 MHz constant clock before a
-// range's first step, so that range starts that much after the range before it and the ranges' launch drains fall
-// apart from the first step (the wait ends on every path: the clock only advances)
-__global__ __launch_bounds__(64) void range_skew_kernel(long long ticks) {
-    const long long t0 = wall_clock64();
-    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(4);
-}
-
 // the launch floor beside a small step (bench.py): an empty launch, and one coalesced load + store per thread
 __global__ __launch_bounds__(1024) void floor_empty_kernel(float *) {}
 __global__ __launch_bounds__(1024) void floor_load_store_kernel(const float *__restrict__ in, float *__restrict__ out) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     out[i] = in[i] + 1.0f;
+}
+// mode 2, a device warm-up (bench.py, after RCCL's initialisation has left the GPU idle for seconds): every thread runs
+// a dependent chain of float32 FMAs and stores its result (in + chain, so the chain cannot be dropped), ~8 us per launch
+// on a full grid at the engine clock; VALU-bound like the step it precedes
+__global__ __launch_bounds__(1024) void floor_busy_kernel(const float *__restrict__ in, float *__restrict__ out) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    float x = in[i], y = 0.5f;
+#pragma unroll 16
+    for (int k = 0; k < 4096; k++) y = __builtin_fmaf(y, 0.99993896484375f, x);
+    out[i] = y;
 }
 
 }  // namespace
@@ -3528,35 +3321,27 @@ int wg_run_ranges(const wg_range *ranges, int32_t n, const wg_params *p, const f
     if (n_steps <= 0) return 0;
     hipStream_t s0 = ranges[0].stream;
     if (n > 1 && hipEventRecord(events[0], s0) != hipSuccess) return fail(WG_EHIP, "fork event record failed");
-    for (int i = 1; i < n; i++)
+    for (int i = 1; i < n; i++)   // (a failed wait leaves nothing issued on the side streams yet: nothing to join)
         if (hipStreamWaitEvent(ranges[i].stream, events[0], 0) != hipSuccess) return fail(WG_EHIP, "fork wait failed");
     // step s of every range is issued before step s + 1 of any: the ranges start together and stay side by side in
     // the hardware queues (range by range, the second range would start only after the host had issued all of the
-    // first range's launches).  WG_RANGE_LEAD: range 0's first `lead` steps issued before the others' first;
-    // WG_RANGE_SKEW_US: range i starts i * skew us after range 0 (range_skew_kernel)
-    const int lead = std::min(std::max(env_int("WG_RANGE_LEAD", 0), 0), (int)n_steps);
-    const long long skew = n_steps > 1 ? std::min(std::max(env_int("WG_RANGE_SKEW_US", 0), 0), 200) * 100ll : 0;
+    // first range's launches).  (Range 0 issued a few steps ahead, or the other ranges started after a timed wait,
+    // measured no better: profiles/r04jj_issue_ab.jsonl.)
     auto issue = [&](int i, int s) -> int {
         const wg_range &r = ranges[i];
-        if (s == 0 && i > 0 && skew > 0) {
-            hipLaunchKernelGGL(range_skew_kernel, dim3(1), dim3(64), 0, r.stream, skew * i);
-            if (hipGetLastError() != hipSuccess) return fail(WG_EHIP, "skew launch failed");
-        }
         return run(r.batch, p, action ? action + r.action_offset : nullptr, action_cols, action_stride, action_step,
                    r.outputs, 1, r.plan, r.plan_blocks, r.stream, true, false, false, s);
     };
-    for (int s = 0; s < lead; s++)
-        if (const int rc = issue(0, s)) return rc;
-    for (int s = 0; s < n_steps; s++) {
-        for (int i = 1; i < n; i++)
-            if (const int rc = issue(i, s)) return rc;
-        if (s + lead < n_steps)
-            if (const int rc = issue(0, s + lead)) return rc;
-    }
+    // A launch-time failure (hipGetLastError after a launch) can still stop the issue part-way, after other ranges or
+    // steps went out: the call then returns that error with a partially stepped batch, but the side streams are joined
+    // back to ranges[0].stream first, so the caller's stream never runs ahead of work the call did issue.
+    int rc = 0;
+    for (int s = 0; s < n_steps && !rc; s++)
+        for (int i = 0; i < n && !rc; i++) rc = issue(i, s);
     for (int i = 1; i < n; i++)
         if (hipEventRecord(events[i], ranges[i].stream) != hipSuccess || hipStreamWaitEvent(s0, events[i], 0) != hipSuccess)
-            return fail(WG_EHIP, "join event failed");
-    return 0;
+            return rc ? rc : fail(WG_EHIP, "join event failed");
+    return rc;
 }
 
 int wg_step_ranges(const wg_range *ranges, int32_t n, const wg_params *p, const float *action, int32_t action_cols,
@@ -3646,14 +3431,16 @@ int wg_plan_ragged(const int32_t *mass_off, const int32_t *edge_off, const int32
 // the launch floor beside a small step (bench.py)
 int wg_launch_floor(int32_t mode, int32_t blocks, int32_t threads, const float *in, float *out, int32_t n_launches,
                     hipStream_t stream) {
-    if (blocks < 1 || threads < 1 || threads > 1024 || n_launches < 0 || (mode != 0 && mode != 1) ||
-        (mode == 1 && (!in || !out)))
+    if (blocks < 1 || threads < 1 || threads > 1024 || n_launches < 0 || mode < 0 || mode > 2 ||
+        (mode >= 1 && (!in || !out)))
         return fail(WG_EINVAL, "bad floor launch (mode %d, %d x %d)", mode, blocks, threads);
     for (int i = 0; i < n_launches; i++) {
         if (mode == 0)
             hipLaunchKernelGGL(floor_empty_kernel, dim3(blocks), dim3(threads), 0, stream, out);
-        else
+        else if (mode == 1)
             hipLaunchKernelGGL(floor_load_store_kernel, dim3(blocks), dim3(threads), 0, stream, in, out);
+        else
+            hipLaunchKernelGGL(floor_busy_kernel, dim3(blocks), dim3(threads), 0, stream, in, out);
     }
     return hipGetLastError() == hipSuccess ? 0 : fail(WG_EHIP, "floor launch failed");
 }

@@ -88,7 +88,7 @@ class DeviceBatch:
         self.wave_ok = bool(wave_ok)
         lean_shape = 4 <= self.M <= 64 and 64 % self.M == 0
         self.ragged = host.ragged
-        self.plan, self.plan_blocks, self.ragged_kind = None, 0, 0
+        self.plan, self.plan_host, self.plan_blocks, self.ragged_kind = None, None, 0, 0
         waves = (wave_ok and self.A <= 64 and L.wg_wave_edge_passes(self.M, self.K) > 0
                  and os.environ.get("WG_LEAN", "1") != "0")
         if (not self.ragged and not lean_shape and waves and os.environ.get("WG_UNIFORM_WAVES", "1") != "0"):
@@ -105,6 +105,7 @@ class DeviceBatch:
             else:
                 nb, self.ragged_kind = _lib.check(L.wg_plan_ragged(*args), "wg_plan_ragged"), 1
             self.plan = _to_dev(plan[:nb + 1], self.device)
+            self.plan_host = plan[:nb + 1].copy()   # block -> first stored walker (walker ranges of plan slices)
             self.plan_blocks = nb
         self.struct = self._make_struct()
 

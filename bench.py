@@ -80,8 +80,9 @@ def parse(argv=None):
     ap.add_argument("--dry-run", action="store_true", help="rank plumbing only (no GPU): every rank reports itself")
     ap.add_argument("--device-warm-ms", type=float, default=None,
                     help="ms of a VALU-bound non-step kernel (wg_launch_floor mode 2) right before the W warm-up steps "
-                         "(default: WG_BENCH_WARM_MS, else 0): RCCL's initialisation idles the GPU for seconds, and steps "
-                         "issued right after that ran slow (DESIGN §8); the line reports it as `device_warm_ms`")
+                         "(default: WG_BENCH_WARM_MS, else 100): the GPU's clocks ramp over ~100 ms of load, and the "
+                         "driver's 20-step region is shorter than that (DESIGN §6); the line reports it as "
+                         "timing.device_warm_ms")
     return ap.parse_args(argv)
 
 
@@ -379,7 +380,7 @@ def main():
         gather_rollout(env.obs, n_total=world * N, dst=dst)
         gather_rollout(rec["reward"], n_total=world * N, dim=1, dst=dst)
         gather_rollout(rec["done"], n_total=world * N, dim=1, dst=dst)
-    warm_ms = args.device_warm_ms if args.device_warm_ms is not None else float(os.environ.get("WG_BENCH_WARM_MS", "0"))
+    warm_ms = args.device_warm_ms if args.device_warm_ms is not None else float(os.environ.get("WG_BENCH_WARM_MS", "100"))
     warm_s = device_warm(stream, dev, warm_ms)
     if args.warmup > 0:
         env.run(acts_w, args.warmup, lanes=lanes)

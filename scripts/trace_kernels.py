@@ -16,6 +16,9 @@ were running at once:
 
     python scripts/trace_kernels.py <run_kernel_trace.csv> --window GRID SKIP COUNT STEPS [out.json [key=value ...]]
 
+(GRID 0: every step launch whose grid is not the largest one — the walker ranges of a ragged batch have grids of their
+own sizes.)
+
 (key=value pairs are stored in the JSON: bench.py picks a window record up by its `workload` and `walkers`.)"""
 import csv
 import json
@@ -32,7 +35,12 @@ def launches(path):
 
 
 def window(path, grid, skip, count, steps):
-    w = [x for x in launches(path) if x[1] == grid][skip:skip + count]
+    allw = list(launches(path))
+    if grid == 0:   # the walker-range launches: every grid but the largest (the full-batch control launches)
+        big = max(x[1] for x in allw)
+        w = [x for x in allw if x[1] != big][skip:skip + count]
+    else:
+        w = [x for x in allw if x[1] == grid][skip:skip + count]
     if len(w) < count:
         raise SystemExit(f"only {len(w)} launches of grid {grid} after skipping {skip}")
     t0, t1 = min(x[2] for x in w), max(x[3] for x in w)
@@ -53,7 +61,7 @@ def window(path, grid, skip, count, steps):
             busy[min(cur, 2)] += t - last
         cur, last = cur + d, t
     span = t1 - t0
-    return {"kernel": w[0][0], "grid_threads": grid, "launches": count, "window": f"launches {skip}..{skip + count - 1}",
+    return {"kernel": w[0][0], "grid_threads": grid if grid else sorted({x[1] for x in w}), "launches": count, "window": f"launches {skip}..{skip + count - 1}",
             "steps": steps, "span_us": round(span / 1e3, 3), "us_per_step": round(span / 1e3 / steps, 4),
             "queues": queues, "share_two_or_more_running": round(busy[2] / span, 4),
             "share_one_running": round(busy[1] / span, 4), "share_idle": round(busy[0] / span, 4)}

@@ -2267,6 +2267,11 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
         // no early loop exit: it keeps er[] in registers (a reference under a `break` made hipcc park the rest
         // lengths in scratch right after their loads, serialising them)
         if (64 * it >= nE) continue;                       // wave-uniform
+        if ((WG_ABLATE & 4096) && it == NE - 1 && it > 0) {   // (ablation: the last spring pass's terms as zeros)
+            const int le = lane + 64 * it;
+            if (le < nE) ts.put(le, 0.0, 0.0, 0.0, 0.f, 0.f, 0.f);
+            continue;
+        }
         Gath g;
         gather(it, g);
         spring(it, g);

@@ -47,15 +47,20 @@ def test_policy_loop_equals_step_loop(lanes, graph):
     assert not torch.equal(acts_seen[1], acts_seen[T - 1])
 
 
-@pytest.mark.parametrize("kind,lanes,graph", [("ragged", 1, False), ("ragged", 2, False), ("ragged", 3, True),
-                                              ("lattice25", 2, False)])
-def test_policy_loop_ragged_equals_step_loop(kind, lanes, graph):
+@pytest.mark.parametrize("kind,lanes,graph,window,contig", [
+    ("ragged", 1, False, "512", [True]),
+    ("ragged", 2, False, "0", [False, False]),             # one global packing: scattered ranges
+    ("ragged", 3, True, "512", [False, False, True]),      # a scattered and a caller-contiguous range together
+    ("ragged", 2, True, "128", [True, True]),              # caller-contiguous ranges
+    ("lattice25", 2, False, "512", [True, True])])         # identity order
+def test_policy_loop_ragged_equals_step_loop(kind, lanes, graph, window, contig, monkeypatch):
     """Mixed-topology batches (stored in wave-tile order) and uniform M = 25 walkers (wave tiles in
-    identity order): each range gathers its caller rows, applies the policy, scatters the actions; the trajectories
-    are bit-identical to `for t: step(policy(obs, t))`."""
+    identity order): a range whose walkers are a contiguous slice of caller rows reads its rows as a slice, a scattered
+    one gathers its rows and scatters its actions; the trajectories are bit-identical to `for t: step(policy(obs, t))`."""
     import torch
     from walker_gym_amd.batched_env import BatchedPhysicsEnv
     from walker_gym_amd.synthetic import canonical_walkers, ragged_walkers
+    monkeypatch.setenv("WG_TILE_WINDOW", window)
     N, T = 3000, 10
     spec = ragged_walkers(N, seed=41, mmin=4, mmax=32) if kind == "ragged" else canonical_walkers(N, seed=5, M=25, K=60,
                                                                                                   A=10)
@@ -69,6 +74,7 @@ def test_policy_loop_ragged_equals_step_loop(kind, lanes, graph):
     for t in range(T):
         ref.step(policy(ref.obs, t))
     env = BatchedPhysicsEnv(spec, device="cuda:0", in3d=1)
+    assert env._caller_bounds(lanes)[1] == contig
     env.policy_loop(policy, T, lanes=lanes, graph=graph)
     torch.cuda.synchronize()
     for name in ("pos", "vel", "acc", "obs", "reward", "done", "centroid", "energy", "muscle_x"):

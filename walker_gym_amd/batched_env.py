@@ -648,10 +648,14 @@ class BatchedPhysicsEnv:
         (no per-step host cost; the policy must be capturable).  After the call obs / reward / done / info hold the last
         step's outputs.
 
-        Ragged batches (stored in wave-tile order, wg_batch.row) run ranges of plan blocks, whose walkers are a
-        scattered set of caller rows: each range gathers its rows of obs (index_select), applies the policy to them and
-        scatters the actions into its rows of one [N, A] action buffer (index_copy_), which its step reads by caller
-        row; the ranges' rows are disjoint, so they still never wait for one another.
+        Ragged batches (stored in wave-tile order, wg_batch.row) run ranges of plan blocks.  The wave tiles are packed
+        within windows of consecutive caller walkers (layout.wave_tile_order), so a range that ends at a block whose
+        stored prefix is exactly the caller rows before it covers a contiguous slice of caller rows: the ranges are
+        split at the such block nearest to an even split (_caller_bounds), and each range reads its obs rows as a
+        slice and hands the kernel its actions as given.  Where no such block is near, a range's walkers are a
+        scattered set of caller rows: it gathers its rows of obs (index_select), applies the policy and scatters the
+        actions into its rows of one [N, A] action buffer (index_copy_), which its step reads by caller row.  Either
+        way the ranges' rows are disjoint, so they never wait for one another.
 
         Host cost per range and step (what bounds a small batch's loop): the policy's own launches, a shape / dtype
         check against the first step's actions, and one C call; the stream is switched only when there are several
@@ -663,20 +667,20 @@ class BatchedPhysicsEnv:
         pref, dev, f32 = C.byref(self._pstruct), self.device, torch.float32
         args = []   # per range: (obs rows or None, row index or None, n_r, batch ref, outputs ref, plan ptr, blocks)
         keep = []   # the ctypes structs the refs point at
-        plan_rows = []   # ragged: the stored walker range [s0, s1) of each range
+        aoff = []   # per range: the caller row its actions start at (the kernel indexes a ragged batch's actions by
+        #             caller row, so a slice's action pointer is moved back by that many rows)
         if b.ragged:
-            nb = b.plan_blocks
-            bb = [nb * i // lanes for i in range(lanes)] + [nb]
+            bb, contiguous = self._caller_bounds(lanes)
             o = self._outputs(self.obs, self.reward, self.done, self.centroid, self.energy, pad_clean=True,
                               steps=self.steps_out, **self._extra_out())
             keep.append(o)
             for i in range(lanes):
                 s0, s1 = int(b.plan_host[bb[i]]), int(b.plan_host[bb[i + 1]])
-                plan_rows.append((s0, s1))
-                if b.row is None:   # identity order (uniform walkers of M not dividing 64): a row slice
+                if contiguous[i]:   # caller rows s0 .. s1 - 1: a row slice
                     obs_r, idx = self.obs[s0:s1], None
-                else:               # the caller rows of stored walkers s0 .. s1 - 1
+                else:               # the caller rows of stored walkers s0 .. s1 - 1, scattered
                     obs_r, idx = None, b._perm["row"][s0:s1]
+                aoff.append(s0)
                 args.append((obs_r, idx, s1 - s0, C.byref(b.struct), C.byref(o),
                              C.c_void_p(b.plan.data_ptr() + 4 * bb[i]), bb[i + 1] - bb[i]))
         else:
@@ -688,6 +692,8 @@ class BatchedPhysicsEnv:
                                   self.energy[w0:w1], pad_clean=True, **self._extra_out(w0, w1))
                 keep += [sub, o]
                 args.append((self.obs[w0:w1], None, w1 - w0, C.byref(sub), C.byref(o), None, 0))
+                aoff.append(0)   # (a sub-batch indexes its actions from its own first walker)
+
         def check(a, n_r):
             require_tensor(a, "policy actions", dev, f32)
             if a.dim() != 2 or a.shape[0] != n_r:
@@ -704,8 +710,8 @@ class BatchedPhysicsEnv:
             sts = [(st, st.cuda_stream) for st in streams]
             shapes = [None] * lanes
             dix = dev.index
-            abuf = None   # ragged: the [N, A] action buffer the ranges scatter into (allocated at the first step, on
-            #               the calling stream, which every range's stream joins at the end)
+            abuf = None   # scattered ragged ranges: the [N, A] action buffer they scatter into (allocated at the first
+            #               step, on the calling stream, which every range's stream joins at the end)
             try:
                 for t in range(int(n_steps)):
                     for r, ((obs_r, idx, n_r, b_ref, o_ref, plan, nblk), (st, st_ptr)) in enumerate(zip(args, sts)):
@@ -724,15 +730,14 @@ class BatchedPhysicsEnv:
                             raise ValueError(f"policy actions changed shape: {tuple(a.shape)} after "
                                              f"{tuple(shapes[r])}")
                         cols = a.shape[1]
-                        if plan is not None:   # ragged: the range's caller rows of the action buffer
+                        if idx is not None:   # a scattered ragged range: its caller rows of the action buffer
                             if abuf is None:
                                 abuf = torch.zeros((self.N, cols), dtype=f32, device=dev)
-                            if idx is None:
-                                abuf[plan_rows[r][0]:plan_rows[r][1]].copy_(a)
-                            else:
-                                abuf.index_copy_(0, idx, a)
-                            a = abuf
-                        rc = step(b_ref, pref, a.data_ptr(), cols, cols, 0, o_ref, 1, plan, nblk, st_ptr)
+                            abuf.index_copy_(0, idx, a)
+                            a_ptr = abuf.data_ptr()
+                        else:                 # (rows aoff[r] .. of the caller's order: the pointer moved back)
+                            a_ptr = a.data_ptr() - 4 * aoff[r] * cols
+                        rc = step(b_ref, pref, a_ptr, cols, cols, 0, o_ref, 1, plan, nblk, st_ptr)
                         if rc:
                             _lib.check(rc, "wg_step")
             finally:
@@ -758,6 +763,30 @@ class BatchedPhysicsEnv:
         g.replay()
         torch.cuda.current_stream(self.device).wait_stream(side)
         self._policy_graph = g   # (kept until the next call: the replay may still be running)
+
+    def _caller_bounds(self, lanes: int):
+        """Plan-block bounds of `lanes` ragged walker ranges, each split moved to the nearest block whose stored prefix
+        holds exactly the caller rows before it (within an eighth of a range), and per range whether its walkers are a
+        contiguous slice of caller rows."""
+        b = self.batch
+        nb, plan = b.plan_blocks, b.plan_host
+        if b.row is None:
+            ok = np.ones(nb + 1, bool)   # identity order: every block boundary
+        else:
+            rowmax = np.maximum.accumulate(b.host.row)
+            ok = np.zeros(nb + 1, bool)
+            ok[0] = ok[nb] = True
+            s = plan[1:nb].astype(np.int64)
+            ok[1:nb] = rowmax[s - 1] == s - 1
+        good = np.flatnonzero(ok)
+        bb = [0]
+        for i in range(1, lanes):
+            t = nb * i // lanes
+            c = int(good[np.argmin(np.abs(good - t))])
+            bb.append(c if abs(c - t) <= max(1, nb // (8 * lanes)) and bb[-1] < c < nb else t)
+        bb.append(nb)
+        contiguous = [bool(ok[bb[i]] and ok[bb[i + 1]]) for i in range(lanes)]
+        return bb, contiguous
 
     def graph(self, actions, n_steps: int, info: bool = True, lanes: Optional[int] = None):
         """Capture run(actions, n_steps) into a HIP graph (torch.cuda.CUDAGraph over the ROCm runtime) and

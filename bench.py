@@ -528,7 +528,8 @@ def main():
             policy_cl = {"policy": ("action = tanh(the walker's own observed muscle lengths), one elementwise kernel "
                                     "per call (row-wise)") if not env.batch.ragged else
                                    ("action = tanh(the first A columns of the walker's own observation row), row-wise; "
-                                    "policy_loop gathers each range's caller rows and scatters its actions"),
+                                    "policy_loop splits the ranges where their walkers are caller-contiguous (a range "
+                                    "elsewhere gathers its rows and scatters its actions)"),
                          "steps": n1,
                          "step_loop_ms_per_step": round(step_pol_ms, 5),
                          "policy_loop_ms_per_step": round(ranges_ms, 5),

@@ -2186,7 +2186,7 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
     // slice: spring terms t (f64 x3) | df (f32 x3) | incidence words | muscle x
     const LeanTerms ts = lean_terms(sl, lg);
 #ifdef WG_STAMPS
-    const int stamp_wave = blockIdx.x * lg.wpb + (threadIdx.x >> 6);
+    const int stamp_wave = t.w0 / lg.wpw;   // (the tile index, as the kernel's own stamps use)
 #endif
     uint32_t *s_inc = reinterpret_cast<uint32_t *>(sl + lg.off_inc);
     float *s_x = reinterpret_cast<float *>(sl + lg.off_x);

@@ -328,12 +328,40 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
+    # RCCL's communicator is created by the first collective that needs it: the rollout-end gather, after the clock
+    # (the pipelined gather, which runs inside the timed region, and WG_COMM_EAGER=1 create it up front).  The timed
+    # region's barriers and the max over ranks go over a gloo group on the host.  Steps issued while a communicator
+    # exists run ~10 % slower in a K = 20 region and not in a K = 1,000 one; `timing.comm_live` times the
+    # same K steps again after the gather, communicator up, so the line carries both.
+    comm_eager = args.gather == "pipelined" or os.environ.get("WG_COMM_EAGER", "0") == "1"
+    ctl = None
+
     def init_group():
+        nonlocal ctl
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            if comm_eager:
+                dist.init_process_group("nccl", device_id=dev)
+            else:
+                dist.init_process_group("nccl")
+                ctl = dist.new_group(backend="gloo")
         else:
             dist.init_process_group(backend)
+
+    def barrier():
+        if ctl is not None:
+            dist.barrier(group=ctl)
+        else:
+            dist.barrier()
+
+    def max_over_ranks(vals):
+        if ctl is not None:
+            t = torch.tensor(vals, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=ctl)
+        else:
+            t = torch.tensor(vals, dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return [float(x) for x in t.tolist()]
 
     # the process group comes up after the env's walker-range streams exist and have run the warm-up: RCCL's own
     # streams then cannot take the hardware queue a side stream would otherwise get (BatchedPhysicsEnv.__init__);
@@ -369,17 +397,24 @@ def main():
     # the rollout SURVEY §8(e) gathers: every step's reward and done flags (written by the steps at per-step offsets,
     # the same bytes as overwriting one row) and the final observations
     rec = None
+    dst = 0 if args.gather_to == "root" else None
+
+    def warm_gather():
+        # one untimed gather of the same tensors, so that the timed one is RCCL's steady state (its first all-gather
+        # of a shape sets up buffers: 0.68 ms against 0.16-0.25 warm at world 1, profiles/r04t_nccl1); the first
+        # collective also creates the communicator
+        gather_rollout(env.obs, n_total=world * N, dst=dst)
+        if rec is not None:
+            gather_rollout(rec["reward"], n_total=world * N, dim=1, dst=dst)
+            gather_rollout(rec["done"], n_total=world * N, dim=1, dst=dst)
+
     if do_gather and graph is None and args.gather != "pipelined":
         rec = {"reward": torch.empty((args.steps, N), dtype=torch.float32, device=dev),
                "done": torch.empty((args.steps, N), dtype=torch.uint8, device=dev),
                "energy": torch.empty((args.steps, N), dtype=torch.float32, device=dev),
                "centroid": torch.empty((args.steps, N, 3), dtype=torch.float32, device=dev)}
-        # one untimed gather of the same tensors, so that the timed one after the steps is RCCL's steady state (its
-        # first all-gather of a shape sets up buffers: 0.68 ms against 0.16-0.25 warm at world 1, profiles/r04t_nccl1)
-        dst = 0 if args.gather_to == "root" else None
-        gather_rollout(env.obs, n_total=world * N, dst=dst)
-        gather_rollout(rec["reward"], n_total=world * N, dim=1, dst=dst)
-        gather_rollout(rec["done"], n_total=world * N, dim=1, dst=dst)
+    if do_gather and comm_eager:
+        warm_gather()
     warm_ms = args.device_warm_ms if args.device_warm_ms is not None else float(os.environ.get("WG_BENCH_WARM_MS", "100"))
     warm_s = device_warm(stream, dev, warm_ms)
     if args.warmup > 0:
@@ -391,7 +426,7 @@ def main():
     prep = env.prepare_run(acts, args.steps, lanes=lanes, record=rec) if graph is None else None
     torch.cuda.synchronize()
     if in_world:
-        dist.barrier()
+        barrier()
     prev_obs = env.obs.clone() if do_gather and args.gather == "pipelined" else None
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -416,23 +451,27 @@ def main():
     # (profiles/r05a_*), which the max over ranks already accounts for
     wall = time.perf_counter() - t0
     if in_world:
-        dist.barrier()
+        barrier()
     torch.cuda.synchronize()
     wall_bar = time.perf_counter() - t0
     step_ms = ev0.elapsed_time(ev1) / args.steps
 
-    wall_t = torch.tensor([wall, wall_bar], dtype=torch.float64, device=dev)
-    if in_world:
-        dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
-    wall_max, wall_bar_max = float(wall_t[0].item()), float(wall_t[1].item())
+    wall_max, wall_bar_max = max_over_ranks([wall, wall_bar]) if in_world else (wall, wall_bar)
     gather_info = None
+    first_gather_ms = None
+    if do_gather and not comm_eager:
+        torch.cuda.synchronize()
+        tf = time.perf_counter()
+        warm_gather()
+        torch.cuda.synchronize()
+        first_gather_ms = max_over_ranks([time.perf_counter() - tf])[0] * 1e3
     if do_gather:
         # the rollout-end gather (RCCL all_gather_into_tensor, shard sizes from shard_bounds) of this
         # rollout's final observations [N, D] and every step's reward and done flags [K, N], right after the barrier
         # that closes the K timed steps, timed on every rank (max): `value` is the K steps (the bench contract),
         # `value_incl_gather` the rollout with its gather.  (Pipelined, opt-in: the previous rollout's observations
         # were gathered while these K steps ran, inside the timed region; the serial gather below then adds none.)
-        dst = 0 if (args.gather_to == "root" and prev_obs is None) else None
+        dst = dst if prev_obs is None else None
         tg_ms = 0.0
         if pending is None:
             torch.cuda.synchronize()
@@ -442,21 +481,37 @@ def main():
                 gathered["reward"] = gather_rollout(rec["reward"], n_total=world * N, dim=1, dst=dst)
                 gathered["done"] = gather_rollout(rec["done"], n_total=world * N, dim=1, dst=dst)
             torch.cuda.synchronize()
-            tg_t = torch.tensor([time.perf_counter() - tg], dtype=torch.float64, device=dev)
-            dist.all_reduce(tg_t, op=dist.ReduceOp.MAX)
-            tg_ms = float(tg_t.item()) * 1e3
+            tg_ms = max_over_ranks([time.perf_counter() - tg])[0] * 1e3
         sent = {"obs": env.obs} if rec is None else {"obs": env.obs, "reward": rec["reward"], "done": rec["done"]}
         gather_info = {"mode": args.gather, "to": ("rank 0 (dist.gather)" if dst == 0 else "every rank (all_gather)"),
                        "rows": world * N, "tensors": sorted(gathered),
                        "bytes_per_rank": int(sum(t.numel() * t.element_size() for t in sent.values())),
                        "gathered_bytes": int(world * sum(t.numel() * t.element_size() for t in sent.values())),
                        "ms": round(tg_ms, 4),
+                       **({"first_gather_ms": round(first_gather_ms, 3),
+                           "first_gather_note": "the untimed gather before it: RCCL's communicator is created here"}
+                          if first_gather_ms is not None else {}),
                        "value_incl_gather": round(world * N * args.steps / (wall_max + tg_ms * 1e-3), 1),
                        "note": "serial (default): this rollout's final observations [N, D] and its per-step reward "
                                "and done flags [K, N], gathered after the barrier closing the K timed steps, into "
                                "every rank (--gather-to root: to rank 0 only), ms = max over ranks; "
                                "value_incl_gather = the K steps and this gather; pipelined (opt-in): the previous "
                                "rollout's final observations gathered while these steps ran (inside the timed region)"}
+
+    comm_live_max = None
+    if in_world and not comm_eager and graph is None:
+        # the same K steps again, now with RCCL's communicator up (the state has advanced; the work is the same):
+        # the rate of a later rollout of an actor that gathers every rollout
+        device_warm(stream, dev, warm_ms)
+        if args.warmup > 0:
+            env.run(acts_w, args.warmup, lanes=lanes)
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        tl = time.perf_counter()
+        prep()
+        torch.cuda.synchronize()
+        comm_live_max = max_over_ranks([time.perf_counter() - tl])[0]
 
     if rank == 0:
         # single-launch control: one full-batch launch per step, HIP events on its stream — the per-dispatch
@@ -575,7 +630,14 @@ def main():
             "timing": {"clock": "wall, t0 after barrier + synchronize, t1 after each rank's synchronize; max over ranks",
                        "ms_per_step_incl_closing_barrier": round(wall_bar_max * 1e3 / args.steps, 5),
                        "device_warm_ms": round(warm_s * 1e3, 2),
-                       "kernel_ms_per_step_events": round(step_ms, 5)},
+                       "kernel_ms_per_step_events": round(step_ms, 5),
+                       **({"comm": "RCCL's communicator created by the first gather, after the timed steps; barriers "
+                                   "and the max over ranks on a gloo group",
+                           "comm_live_ms_per_step": round(comm_live_max * 1e3 / args.steps, 5),
+                           "comm_live_value": round(world * N * args.steps / comm_live_max, 1),
+                           "comm_live_note": "the same K steps timed again after the gather, communicator up, same "
+                                             "warm-up (DESIGN §8)"} if comm_live_max is not None else
+                          {"comm": "RCCL's communicator created before the timed steps"} if in_world else {})},
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,

@@ -38,7 +38,7 @@ class OrcBatch(C.Structure):
                 ("ei", _i32p), ("ej", _i32p), ("rest", _f32p), ("k", _f32p), ("c", _f32p),
                 ("flags", _u8p), ("mx", _f32p), ("minl", _f32p), ("maxl", _f32p), ("stride", _f32p),
                 ("steps", _i32p), ("contact", _u8p), ("pinned", _u8p),
-                ("charge", _f64p), ("radius", _f64p)]
+                ("charge", _f64p), ("radius", _f64p), ("bounce_set", _u8p)]
 
 
 class OrcOut(C.Structure):
@@ -130,6 +130,8 @@ class Oracle:
         rad = s.get("radius")
         self.radius = (self.m.astype(np.float64) ** 0.3 if rad is None
                        else np.ascontiguousarray(rad, np.float64)).copy()
+        bs = s.get("bounce_set")   # Point.bounce(k, other=<list>): bit 0 caller, bit 1 in the list (None: all, "*")
+        self.bounce_set = None if bs is None else np.ascontiguousarray(bs, np.uint8).reshape(-1).copy()
         self.n_threads = n_threads
         Ms = np.diff(self.mass_off)
         d = 3 if P["in3d"] else 2
@@ -149,7 +151,7 @@ class Oracle:
             _p(self.ei, _i32p), _p(self.ej, _i32p), _p(self.rest, _f32p), _p(self.k, _f32p),
             _p(self.c, _f32p), _p(self.flags, _u8p), _p(self.mx, _f32p), _p(self.minl, _f32p),
             _p(self.maxl, _f32p), _p(self.stride, _f32p), _p(self.steps, _i32p), _p(self.contact, _u8p),
-            _p(self.pinned, _u8p), _p(self.charge, _f64p), _p(self.radius, _f64p))
+            _p(self.pinned, _u8p), _p(self.charge, _f64p), _p(self.radius, _f64p), _p(self.bounce_set, _u8p))
 
     def set_params(self, **kw):
         """Change env parameters between steps (the state stays), as BatchedPhysicsEnv.set_params."""

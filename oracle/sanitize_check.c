@@ -19,7 +19,7 @@ static float unif(float a, float b) { return a + (b - a) * (float)(rnd() % 10000
 static void *xmalloc(size_t n) { void *p = malloc(n ? n : 1); if (!p) { perror("malloc"); exit(2); } return p; }
 
 static int run_case(int N, int spring_mode, int pair_mode, int integrator, int action_mode, int friction_mode,
-                    int in3d, int conmid) {
+                    int in3d, int conmid, int subset) {
     int32_t *mass_off = xmalloc(sizeof(int32_t) * (N + 1)), *edge_off = xmalloc(sizeof(int32_t) * (N + 1));
     int32_t *muscle_off = xmalloc(sizeof(int32_t) * (N + 1));
     mass_off[0] = edge_off[0] = muscle_off[0] = 0;
@@ -34,7 +34,9 @@ static int run_case(int N, int spring_mode, int pair_mode, int integrator, int a
     float *m = xmalloc(sizeof(float) * P);
     uint8_t *contact = xmalloc(P), *pinned = xmalloc(P);
     double *charge = xmalloc(sizeof(double) * P), *radius = xmalloc(sizeof(double) * P);
+    uint8_t *bounce_set = subset ? xmalloc(P) : NULL;   /* Point.bounce(k, other=<list>): caller / list bits */
     for (int i = 0; i < P; i++) {
+        if (bounce_set) bounce_set[i] = (uint8_t)(rnd() & 3);
         for (int c = 0; c < 3; c++) { pos[3 * i + c] = unif(-20.f, 20.f); vel[3 * i + c] = unif(-1.f, 1.f); acc[3 * i + c] = 0.f; }
         if (!in3d) { pos[3 * i + 2] = 0.f; vel[3 * i + 2] = 0.f; }
         m[i] = unif(0.5f, 5.f);
@@ -86,7 +88,7 @@ static int run_case(int N, int spring_mode, int pair_mode, int integrator, int a
     p.g3_gravity[1] = -9.8; p.g3_damping = 0.99; p.g3_air = 0.01; p.g3_ground_level = -50; p.g3_restitution = 0.8;
     p.g3_friction = 0.5; p.g3_ground = 1; p.friction_mode = friction_mode;
     orc_batch b = {N, mass_off, edge_off, muscle_off, pos, vel, acc, m, ei, ej, rest, k, c, flags, mx, minl, maxl,
-                   stride, steps, contact, pinned, charge, radius};
+                   stride, steps, contact, pinned, charge, radius, bounce_set};
     orc_out o = {obs, Dmax, reward, done, centroid, energy};
     int rc = orc_reset(&b, &p, noise, 1);
     for (int s = 0; s < 8 && rc == 0; s++) {
@@ -96,10 +98,11 @@ static int run_case(int N, int spring_mode, int pair_mode, int integrator, int a
     if (rc == 0) rc = orc_observe(&b, &p, &o, 1);
     int finite = 0;
     for (int i = 0; i < N; i++) finite += isfinite(reward[i]) != 0;
-    printf("case spring=%d pair=%d run%d act=%d fric=%d in3d=%d conmid=%d: rc=%d, %d/%d finite rewards\n", spring_mode,
-           pair_mode, integrator == 2 ? 2 : 1, action_mode, friction_mode, in3d, conmid, rc, finite, N);
+    printf("case spring=%d pair=%d%s run%d act=%d fric=%d in3d=%d conmid=%d: rc=%d, %d/%d finite rewards\n",
+           spring_mode, pair_mode, subset ? " (bounce subset)" : "", integrator == 2 ? 2 : 1, action_mode, friction_mode,
+           in3d, conmid, rc, finite, N);
     free(mass_off); free(edge_off); free(muscle_off); free(pos); free(vel); free(acc); free(m); free(contact);
-    free(pinned); free(charge); free(radius); free(ei); free(ej); free(rest); free(k); free(c); free(flags); free(mx);
+    free(pinned); free(charge); free(radius); free(bounce_set); free(ei); free(ej); free(rest); free(k); free(c); free(flags); free(mx);
     free(minl); free(maxl); free(stride); free(steps); free(action); free(obs); free(reward); free(done);
     free(centroid); free(energy); free(noise);
     return rc;
@@ -107,11 +110,12 @@ static int run_case(int N, int spring_mode, int pair_mode, int integrator, int a
 
 int main(void) {
     int bad = 0;
-    bad |= run_case(60, 0, 0, 1, 0, 0, 1, 0) != 0;
-    bad |= run_case(60, 0, 7, 1, 0, 0, 1, 1) != 0;
-    bad |= run_case(60, 1, 0, 2, 1, 0, 0, 0) != 0;
-    bad |= run_case(60, 2, 0, 1, 0, 0, 1, 0) != 0;
-    bad |= run_case(60, 0, 3, 2, 0, 1, 0, 1) != 0;
+    bad |= run_case(60, 0, 0, 1, 0, 0, 1, 0, 0) != 0;
+    bad |= run_case(60, 0, 7, 1, 0, 0, 1, 1, 0) != 0;
+    bad |= run_case(60, 0, 4, 1, 0, 0, 1, 0, 1) != 0;
+    bad |= run_case(60, 1, 0, 2, 1, 0, 0, 0, 0) != 0;
+    bad |= run_case(60, 2, 0, 1, 0, 0, 1, 0, 0) != 0;
+    bad |= run_case(60, 0, 3, 2, 0, 1, 0, 1, 0) != 0;
     printf(bad ? "FAILED\n" : "sanitize ok\n");
     return bad;
 }

@@ -26,7 +26,7 @@
 #include <omp.h>
 #endif
 
-#define ORC_ABI 4
+#define ORC_ABI 5
 int orc_abi_version(void) { return ORC_ABI; }
 
 /* Config.r (gym/engine.py:9, gym/optimized_engine.py:7): the distance clamp, a Python float. */
@@ -266,12 +266,15 @@ static void walker_step(const orc_batch *b, const orc_params *p, int w, const fl
     /*     Bounce: for s in registry order, for every other point i (gym/engine.py:114-125): if
      *     norm(s.pos - i.pos).astype(float) <= s.r + i.r: s.resilience(i, s.r + i.r, k / 2) (:78-102),
      *     a rigid spring of rest x = s.r + i.r (Python float, weakly cast to float32 in dx = current - x)
-     *     and stiffness k/2 (float32 in f_size = -dx * k), applied to s then to i as in the spring pass. */
+     *     and stiffness k/2 (float32 in f_size = -dx * k), applied to s then to i as in the spring pass.
+     *     With a bounce_set, only the callers s (bit 0) bounce, each against `other` = the points with bit 1. */
     if (p->pair_mode & 4) {
         const float kb = (float)(p->bounce_k / 2);
-        for (int s = m0; s < m1; s++)
+        const uint8_t *bs = b->bounce_set;
+        for (int s = m0; s < m1; s++) {
+            if (bs && !(bs[s] & 1)) continue;
             for (int i = m0; i < m1; i++) {
-                if (i == s) continue;
+                if (i == s || (bs && !(bs[i] & 2))) continue;
                 const float *ps = pos + 3 * s, *pi = pos + 3 * i;
                 const double x = b->radius[s] + b->radius[i];
                 const float cur = np_norm3(ps[0] - pi[0], ps[1] - pi[1], ps[2] - pi[2]);
@@ -283,6 +286,7 @@ static void walker_step(const orc_batch *b, const orc_params *p, int w, const fl
                 for (int c = 0; c < 3; c++) acc[3 * s + c] = add_f64(acc[3 * s + c], (double)(nf * (pi[c] - ps[c])) / dist, b->m[s]);
                 for (int c = 0; c < 3; c++) acc[3 * i + c] = add_f64(acc[3 * i + c], (double)(nf * (ps[c] - pi[c])) / dist, b->m[i]);
             }
+        }
     }
     /*     G2 Point.gravity = gravity_vec (gym/optimized_engine.py:167-197; the performance_demo loop's N-body,
      *     gym/performance_demo.py:52-58): with >= 2 points every a is zeroed first (:174-175, discarding the

@@ -22,7 +22,7 @@ typedef struct orc_params {
     int32_t integrator;    /* 0/1 = Point.run1 (gym/engine.py:168-178); 2 = Point.run2 (:180-190) */
     int32_t pair_mode;     /* bitmask, per walker after the springs, in this order: 1 = Point.gravity
                               (gym/engine.py:128-137), 2 = Point.coulomb (:139-147), 4 = Point.bounce
-                              for every point in registry order (:114-125) */
+                              of every caller in registry order against its `other` set (:114-125) */
     double pair_g;         /* Config.g of the gravity pass (gym/engine.py:12) */
     double pair_k;         /* Config.k of the coulomb pass (gym/engine.py:11) */
     double pair_e;         /* Point.e when charge == NULL (Config.e, gym/engine.py:10) */
@@ -52,6 +52,9 @@ typedef struct orc_batch {
     double *radius;                  /* [P] Point.r (Python floats), read by bounce; the env pass sets
                                         3 on contact, 1 otherwise (optimized_env.py:156,175); may be NULL
                                         unless pair_mode & 4 */
+    const uint8_t *bounce_set;       /* [P] Point.bounce(k, other=<list>) (gym/engine.py:114-125): bit 0 = the point
+                                        calls bounce (callers in registry order), bit 1 = the point is in `other`
+                                        (the list in registry order); NULL = every point, other="*" */
 } orc_batch;
 
 typedef struct orc_out {

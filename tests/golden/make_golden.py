@@ -121,8 +121,10 @@ class Spec:
     """A batch in the flat CSR layout used by the oracle and the GPU path."""
 
     def __init__(self, m, pos, vel, mass_off, ei, ej, rest, k, c, flags, edge_off, n_muscles,
-                 minl, maxl, stride, acc=None, pinned=None, mx=None, charge=None, radius=None):
+                 minl, maxl, stride, acc=None, pinned=None, mx=None, charge=None, radius=None, bounce_set=None):
         self.m = np.asarray(m, np.float32)
+        # Point.bounce(k, other=<list>) per point: bit 0 calls bounce, bit 1 is in the list (None: every point, "*")
+        self.bounce_set = None if bounce_set is None else np.asarray(bounce_set, np.uint8)
         self.charge = None if charge is None else np.asarray(charge, np.float64)   # Point.e
         self.radius = None if radius is None else np.asarray(radius, np.float64)   # Point.r
         self.pos = np.asarray(pos, np.float32).reshape(-1, 3)
@@ -150,7 +152,7 @@ class Spec:
         for key in ("m", "pos", "vel", "acc", "mass_off", "ei", "ej", "rest", "k", "c", "flags",
                     "edge_off", "n_muscles", "minl", "maxl", "stride"):
             d[prefix + key] = getattr(self, key)
-        for key in ("charge", "radius"):
+        for key in ("charge", "radius", "bounce_set"):
             if getattr(self, key) is not None:
                 d[prefix + key] = getattr(self, key)
         if self.pinned.any():
@@ -239,8 +241,15 @@ class RefRun:
                 if P["pair_mode"] & 2:
                     E.Point.coulomb()              # :139-147
                 if P["pair_mode"] & 4:
-                    for p in cr.phys:              # :114-125, registry order
-                        p.bounce(P["bounce_k"])
+                    bits = [getattr(p, "_golden_bounce", 3) for p in cr.phys]
+                    if all(b == 3 for b in bits):
+                        for p in cr.phys:          # :114-125, registry order, other = "*"
+                            p.bounce(P["bounce_k"])
+                    else:                          # the callers in registry order, each against one list
+                        other = [p for p, b in zip(cr.phys, bits) if b & 2]
+                        for p, b in zip(cr.phys, bits):
+                            if b & 1:
+                                p.bounce(P["bounce_k"], other=other)
                 if P["pair_mode"] & 8:             # G2 Point.gravity = gravity_vec (gym/optimized_engine.py:167-197)
                     OEng = sys.modules["optimized_engine"]
                     saved2, og = OEng.Point.points, OEng.Config.g
@@ -385,6 +394,8 @@ def creatures_from_spec(E, OW, spec: Spec):
                 p.e = float(spec.charge[q])
             if spec.radius is not None:
                 p.r = float(spec.radius[q])
+            if spec.bounce_set is not None:
+                p._golden_bounce = int(spec.bounce_set[q])   # (read by RefRun.physics, not by the reference)
             phys.append(p)
         for q, p in zip(range(a, b), phys):
             p.old_a = spec.acc[q].copy()
@@ -699,6 +710,30 @@ def sc_pairs(c):
         crs = creatures_from_spec(c.E, c.OW, spec)
         acts = rng.uniform(-1, 1, (60, spec.N, A)).astype(f32)
         c.save(name, RefRun(c.E, c.OW, c.OE, crs, dict(in3d=in3d, pair_mode=pm, **extra_p)), spec, 60, acts)
+
+
+@scenario("pair_bounce_subset_canonical", "pair_bounce_subset_lattice25")
+def sc_bounce_subset(c):
+    """O2. Point.bounce(k, other=<list>) (gym/engine.py:114-125) with a proper subset: on each walker the points with
+    bit 0 call p.bounce(k, other=L) in registry order, L = the points with bit 1 in registry order (bits U{0..3} per
+    point, so callers outside L, L members that never call, and both); the shrunk canonical lattice (lean kernel) and a
+    shrunk 25-mass lattice (workgroup kernel), radii U(1.5, 3), 60 steps."""
+    def shrunk25(seed):
+        sp = canonical_walkers(3, seed=seed, M=25, K=60, A=10)
+        sp["pos"] = (sp["pos"] * np.float32(0.4)).astype(f32)
+        sp["rest"] = (sp["rest"] * np.float32(0.4)).astype(f32)
+        return sp
+    cases = (("pair_bounce_subset_canonical", lambda r: Spec(**_shrunk(59), radius=r.uniform(1.5, 3.0, 48),
+                                                            bounce_set=r.integers(0, 4, 48)), 8),
+             ("pair_bounce_subset_lattice25", lambda r: Spec(**shrunk25(61), radius=r.uniform(1.5, 3.0, 75),
+                                                            bounce_set=r.integers(0, 4, 75)), 10))
+    for name, mk, A in cases:
+        rng = scenario_rng(name)
+        c.fresh()
+        spec = mk(rng)
+        crs = creatures_from_spec(c.E, c.OW, spec)
+        acts = rng.uniform(-1, 1, (60, spec.N, A)).astype(f32)
+        c.save(name, RefRun(c.E, c.OW, c.OE, crs, dict(in3d=1, pair_mode=4, bounce_k=2000.0)), spec, 60, acts)
 
 
 @scenario(*[f"chain_engine_gravity_{n}" for n in (10, 50, 100, 200)])

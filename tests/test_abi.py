@@ -52,7 +52,7 @@ int main(void) {
          sizeof(wg_params), sizeof(wg_batch), sizeof(wg_outputs), sizeof(wg_edge), sizeof(wg_launch_info));
   F(wg_batch, pos) F(wg_batch, edges) F(wg_batch, inc_off) F(wg_batch, muscle_bounds) F(wg_batch, contact)
   F(wg_outputs, obs_step) F(wg_outputs, out_step) F(wg_params, in3d) F(wg_params, action_mode) F(wg_params, pair_g)
-  F(wg_params, bounce_k) F(wg_batch, charge) F(wg_batch, radius)
+  F(wg_params, bounce_k) F(wg_batch, charge) F(wg_batch, radius) F(wg_batch, row) F(wg_batch, bounce_set)
   printf("wg_range %zu\\n", sizeof(wg_range));
   F(wg_range, outputs) F(wg_range, action_offset) F(wg_range, plan) F(wg_range, plan_blocks) F(wg_range, stream)
   return 0;

@@ -172,7 +172,7 @@ def test_imported_topologies_vs_oracle():
         _oracle_compare(spec, params, 20, acts)
 
 
-@pytest.mark.parametrize("pair_mode", [7, 24, 31])
+@pytest.mark.parametrize("pair_mode", [7, 24, 31, "4_subset", "31_subset"])
 def test_pair_forces_4096_vs_oracle(pair_mode):
     """pair_mode bits in order (gravity, coulomb, bounce of gym/engine.py:114-147; 8 G2 gravity_vec,
     gym/optimized_engine.py:167-197; 16 electrostatic, gym/engine.py:150-158), per walker on the lean kernel, on 4096
@@ -187,6 +187,9 @@ def test_pair_forces_4096_vs_oracle(pair_mode):
     rng = np.random.default_rng(5)
     spec["charge"] = rng.uniform(-3, 3, 16 * N)
     spec["radius"] = rng.uniform(1.5, 3.0, 16 * N)
+    if isinstance(pair_mode, str):   # Point.bounce(k, other=<list>): random caller / list bits (wg_batch.bounce_set)
+        pair_mode = int(pair_mode.split("_")[0])
+        spec["bounce_set"] = rng.integers(0, 4, 16 * N).astype(np.uint8)
     params = dict(in3d=1, pair_mode=pair_mode, pair_g=2000.0, pair_k=1.0e4, bounce_k=2000.0)
     acts = rng.uniform(-1, 1, (20, N, 8)).astype(np.float32)
     env, orc = _oracle_compare(spec, params, 20, acts, rtol=0, atol=0)

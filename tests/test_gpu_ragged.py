@@ -108,9 +108,10 @@ def test_wave_kernel_dense_walkers_vs_oracle():
     assert np.array_equal(env.muscle_x.cpu().numpy(), orc.mx)
 
 
-@pytest.mark.parametrize("pair_mode", [7, 31])
+@pytest.mark.parametrize("pair_mode", [7, 31, "4_subset"])
 @pytest.mark.parametrize("case", ["ragged", "uniform_M13", "uniform_M100", "uniform_M100_wide"])
 def test_pair_forces_workgroup_kernel_vs_oracle(case, pair_mode):
+    """4_subset: Point.bounce(k, other=<list>) with random caller / list bits per point (wg_batch.bounce_set)."""
     import torch
     from oracle.oracle import Oracle
     from walker_gym_amd.batched_env import BatchedPhysicsEnv
@@ -128,6 +129,9 @@ def test_pair_forces_workgroup_kernel_vs_oracle(case, pair_mode):
     P = int(spec["mass_off"][-1])
     spec["charge"] = rng.uniform(-3, 3, P)
     spec["radius"] = rng.uniform(0.5, 2.0, P)
+    if pair_mode == "4_subset":
+        pair_mode = 4
+        spec["bounce_set"] = rng.integers(0, 4, P).astype(np.uint8)
     N = len(spec["mass_off"]) - 1
     A = max(1, int(np.max(spec["n_muscles"])))
     params = dict(in3d=1, pair_mode=pair_mode, pair_g=500.0, pair_k=2.0e3, bounce_k=400.0)

@@ -1,5 +1,6 @@
 """Host packing: incidence lists reproduce the reference accumulation order; encodings; byte model."""
 import numpy as np
+import pytest
 
 from walker_gym_amd.layout import algorithmic_bytes_per_walker_step, incidence, pack
 from walker_gym_amd.synthetic import canonical_walkers, norm3_f32, ragged_walkers
@@ -206,3 +207,27 @@ def test_wave_tile_order_windows_keep_caller_locality():
     for s in range(0, 5000, 512):
         assert sorted(win[s:s + 512].tolist()) == list(range(s, min(s + 512, 5000)))
     assert ntiles(win) <= 1.01 * ntiles(glob), (ntiles(win), ntiles(glob))
+
+
+def test_bounce_set_packing():
+    """ABI 12: Point.bounce(k, other=<list>) per point as bit 0 (calls) | bit 1 (in the list); all 3 (other="*") is
+    stored as None, entries outside 0..3 and a wrong length are refused; a ragged batch's copy follows its walkers
+    into stored order."""
+    from walker_gym_amd.layout import pack
+    from walker_gym_amd.synthetic import canonical_walkers, ragged_walkers
+    spec = canonical_walkers(5, seed=1)
+    P = int(spec["mass_off"][-1])
+    assert pack(spec).bounce_set is None
+    assert pack(dict(spec, bounce_set=np.full(P, 3, np.uint8))).bounce_set is None
+    bs = np.random.default_rng(0).integers(0, 4, P).astype(np.uint8)
+    assert np.array_equal(pack(dict(spec, bounce_set=bs)).bounce_set, bs)
+    with pytest.raises(ValueError):
+        pack(dict(spec, bounce_set=np.full(P, 4, np.uint8)))
+    with pytest.raises(ValueError):
+        pack(dict(spec, bounce_set=bs[:-1]))
+    rg = ragged_walkers(300, seed=3, mmin=3, mmax=40)
+    Pr = int(rg["mass_off"][-1])
+    bsr = np.random.default_rng(1).integers(0, 4, Pr).astype(np.uint8)
+    lay = pack(dict(rg, bounce_set=bsr))
+    assert np.array_equal(lay.bounce_set[lay.mass_perm], bsr) if lay.mass_perm is not None else \
+        np.array_equal(lay.bounce_set, bsr)

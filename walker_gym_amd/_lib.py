@@ -13,7 +13,7 @@ import threading
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libwalker_hip.so"
 LIB_PATH = os.path.join(HERE, LIB_NAME)
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 WG_EINVAL, WG_ERANGE, WG_EHIP = -1, -2, -3
 
@@ -40,7 +40,7 @@ class WgBatch(C.Structure):
                 ("inc", _vp), ("inc_off", _vp),
                 ("muscle_x", _vp), ("muscle_bounds", _vp), ("muscle_stride", _vp),
                 ("steps", _vp), ("contact", _vp), ("pinned", _vp),
-                ("charge", _vp), ("radius", _vp), ("row", _vp)]
+                ("charge", _vp), ("radius", _vp), ("row", _vp), ("bounce_set", _vp)]
 
 
 class WgOutputs(C.Structure):

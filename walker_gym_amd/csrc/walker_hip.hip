@@ -1309,9 +1309,13 @@ __device__ void pair_forces_lds(const wg_batch &b, const KParams &kp, const floa
                                      g0, kp.pair_e, md, ym, p3, ax, ay, az);
     if (kp.pair_mode & 4) {                  // gym/engine.py:114-125, partners j < q, then j != q, then j > q
         const double rs = b.radius[g0 + q];
+        // bounce_set: bit 0 calls bounce, bit 1 is in `other` (pair_bounce, lean kernel); NULL = every point both
+        const int bs = b.bounce_set ? (int)b.bounce_set[g0 + q] : 3;
         for (int ph = 0; ph < 3; ph++) {
             for (int pj = 0; pj < M; pj++) {
-                const bool on = ph == 0 ? pj < q : ph == 1 ? pj != q : pj > q;
+                const int obs = b.bounce_set ? (int)b.bounce_set[g0 + pj] : 3;
+                const bool on = ph == 1 ? pj != q && (bs & 1) && (obs & 2)
+                                        : (ph == 0 ? pj < q : pj > q) && (obs & 1) && (bs & 2);
                 if (!on) continue;
                 const float *o3 = spos + 3 * (lm + pj);
                 const float d0 = o3[0] - p3[0], d1 = o3[1] - p3[1], d2 = o3[2] - p3[2];
@@ -2099,7 +2103,10 @@ __device__ __forceinline__ void pair_central(double coef, double sq, const float
 // depend on which end is s (norm and r_s + r_i are symmetric), so mass q receives, in the reference's order:
 // every partner j < q (outer loop at j), then every partner j != q ascending (outer loop at q), then every
 // partner j > q (outer loop at j).  rs = this lane's Point.r (the env pass overwrites it with 3 / 1).
-__device__ __forceinline__ void pair_bounce(float kh, double rs, const float *p3, float mf, int lane, int M,
+// With a bounce_set (Point.bounce(k, other=<list>) on a subset of callers): bs = this lane's bits (1 calls, 2 in the
+// list); q receives, in the same three phases, the terms of callers j < q when q is listed, its own call's terms
+// against the listed j != q when q calls, then the terms of callers j > q when q is listed (bs = 3: every point).
+__device__ __forceinline__ void pair_bounce(float kh, double rs, int bs, const float *p3, float mf, int lane, int M,
                                             bool is_mass, float &ax, float &ay, float &az) {
     const int gb = lane & ~(M - 1), q = lane & (M - 1);
     const double md = (double)mf, ym = 1.0 / md;
@@ -2108,7 +2115,9 @@ __device__ __forceinline__ void pair_bounce(float kh, double rs, const float *p3
             const int src = (gb + pj) << 2;
             const float ox = lane_gather(p3[0], src), oy = lane_gather(p3[1], src), oz = lane_gather(p3[2], src);
             const double orad = lane_gather_d(rs, src);
-            const bool on = ph == 0 ? pj < q : ph == 1 ? pj != q : pj > q;
+            const int obs = __builtin_amdgcn_ds_bpermute(src, bs);
+            const bool on = ph == 1 ? pj != q && (bs & 1) && (obs & 2)
+                                    : (ph == 0 ? pj < q : pj > q) && (obs & 1) && (bs & 2);
             if (!is_mass || !on) continue;
             const float d0 = ox - p3[0], d1 = oy - p3[1], d2 = oz - p3[2];   // partner - self
             const float cur = np_norm3(d0, d1, d2);
@@ -2151,7 +2160,8 @@ __device__ __forceinline__ void pair_forces(const wg_batch &b, const KParams &kp
     }
     if (kp.pair_mode & 4) {
         const double rs = is_mass ? b.radius[pl] : 0.0;
-        pair_bounce(kp.bounce_kh, rs, p3, mf, lane, M, is_mass, ax, ay, az);
+        const int bs = b.bounce_set ? (is_mass ? (int)b.bounce_set[pl] : 0) : 3;
+        pair_bounce(kp.bounce_kh, rs, bs, p3, mf, lane, M, is_mass, ax, ay, az);
     }
     if (kp.pair_mode & 8) pair_g2_gravity(kp.pair_g, p3, mf, lane, M, is_mass, ax, ay, az);
     if (kp.pair_mode & 16) {

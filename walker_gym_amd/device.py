@@ -59,6 +59,7 @@ class DeviceBatch:
         self.contact = torch.zeros(self.P, dtype=torch.uint8, device=dv) if contact else None
         self.pinned = _to_dev(host.pinned, dv) if host.pinned is not None else None
         self.charge = _to_dev(host.charge, dv) if host.charge is not None else None
+        self.bounce_set = _to_dev(host.bounce_set, dv) if host.bounce_set is not None else None
         self.radius = None   # allocated by enable_radius(): the step writes it, so only when bounce needs it
         # placeholders so that zero-size arrays still have a valid device pointer
         self._dummy = torch.zeros(16, dtype=torch.float32, device=dv)
@@ -159,7 +160,8 @@ class DeviceBatch:
             inc=self._p(self.inc) if self.inc is not None else None, inc_off=self._p(self.inc_off),
             muscle_x=self._p(self.muscle_x), muscle_bounds=self._p(self.muscle_bounds),
             muscle_stride=self._p(self.muscle_stride), steps=self._p(self.steps), contact=self._p(self.contact),
-            pinned=self._p(self.pinned), charge=self._p(self.charge), radius=self._p(self.radius))
+            pinned=self._p(self.pinned), charge=self._p(self.charge), radius=self._p(self.radius),
+            bounce_set=self._p(self.bounce_set))
 
     def sub_struct(self, w0: int, w1: int) -> _lib.WgBatch:
         """A WgBatch view of walkers [w0, w1) of a uniform batch: the same device memory, pointers offset
@@ -183,7 +185,8 @@ class DeviceBatch:
             muscle_bounds=self._p(self.muscle_bounds) if A == 0 else off(self.muscle_bounds, 2 * A * w0),
             muscle_stride=self._p(self.muscle_stride) if A == 0 else off(self.muscle_stride, A * w0),
             steps=off(self.steps, w0), contact=off(self.contact, M * w0), pinned=off(self.pinned, M * w0),
-            charge=off(self.charge, M * w0), radius=off(self.radius, M * w0), row=None)
+            charge=off(self.charge, M * w0), radius=off(self.radius, M * w0), row=None,
+            bounce_set=off(self.bounce_set, M * w0))
 
     def launch_geometry(self) -> dict:
         info = _lib.WgLaunchInfo()

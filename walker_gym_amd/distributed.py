@@ -36,7 +36,7 @@ def shard_spec(spec: dict, start: int, stop: int) -> dict:
     uo = np.concatenate([[0], np.cumsum(nm)])
     p0, p1, e0, e1, u0, u1 = mo[start], mo[stop], eo[start], eo[stop], uo[start], uo[stop]
     out = {}
-    for k in ("m", "pos", "vel", "acc", "pinned", "charge", "radius"):
+    for k in ("m", "pos", "vel", "acc", "pinned", "charge", "radius", "bounce_set"):
         if k in spec:
             out[k] = np.asarray(spec[k])[p0:p1]
     for k in ("ei", "ej", "rest", "k", "c", "flags"):

@@ -53,6 +53,9 @@ class HostLayout:
     pinned: Optional[np.ndarray] = None   # uint8 [P]: DingPoint masses (None = no pinned mass)
     charge: Optional[np.ndarray] = None   # float64 [P]: Point.e (None = Config.e for every point)
     radius: Optional[np.ndarray] = None   # float64 [P]: Point.r (None = m ** 0.3, gym/engine.py:45-46)
+    # uint8 [P]: Point.bounce(k, other=<list>) (gym/engine.py:114-125): bit 0 = calls bounce, bit 1 = in the list
+    # (None = every point calls, other="*")
+    bounce_set: Optional[np.ndarray] = None
     # ragged batches are stored in wave-tile / size order (size_order): row [N] = the caller's index of each stored walker, mass_perm /
     # muscle_perm = the stored index of each caller mass / muscle (None = stored in the caller's order)
     row: Optional[np.ndarray] = None
@@ -203,6 +206,7 @@ def _pack(spec: Dict[str, np.ndarray], mx: Optional[np.ndarray], steps: Optional
         pinned=_pinned(spec, int(mass_off[-1])),
         charge=_per_mass_f64(spec, "charge", int(mass_off[-1])),
         radius=_per_mass_f64(spec, "radius", int(mass_off[-1])),
+        bounce_set=_bounce_set(spec, int(mass_off[-1])),
     )
 
 
@@ -220,6 +224,22 @@ def _per_mass_f64(spec, key: str, P: int):
 def default_radius(mass: np.ndarray) -> np.ndarray:
     """Point.__init__ radius r = m ** 0.3 (gym/engine.py:45-46), m the stored float32 mass as a Python float."""
     return np.asarray(mass, np.float32).astype(np.float64) ** 0.3
+
+
+def _bounce_set(spec, P: int):
+    """Per point, which side of Point.bounce(k, other=<list>) it is on: bit 0 the point calls bounce (callers in
+    registry order), bit 1 it is in `other` (the list in registry order); other bits must be 0.  All 3 is the
+    reference's default other="*" and is stored as None."""
+    bs = spec.get("bounce_set")
+    if bs is None:
+        return None
+    bs = np.ascontiguousarray(bs).reshape(-1)
+    if bs.shape[0] != P:
+        raise ValueError(f"bounce_set has {bs.shape[0]} entries for {P} masses")
+    if bs.size and (bs.min() < 0 or bs.max() > 3):
+        raise ValueError("bounce_set entries are bit 0 (calls bounce) | bit 1 (in the other list): 0..3")
+    bs = bs.astype(np.uint8)
+    return None if bool(np.all(bs == 3)) else bs.copy()
 
 
 def _pinned(spec, P: int):
@@ -249,7 +269,7 @@ def reorder_walkers(spec: Dict[str, np.ndarray], order: np.ndarray) -> Dict[str,
     eidx, new_eo = gather(eo)
     uidx, _ = gather(uo)
     out = dict(spec)
-    for k in ("m", "pos", "vel", "acc", "pinned", "charge", "radius"):
+    for k in ("m", "pos", "vel", "acc", "pinned", "charge", "radius", "bounce_set"):
         if spec.get(k) is not None:
             out[k] = np.asarray(spec[k])[pidx]
     for k in ("ei", "ej", "rest", "k", "c", "flags"):

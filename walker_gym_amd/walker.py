@@ -139,7 +139,7 @@ def replicate_spec(spec: dict, n: int) -> dict:
         raise ValueError("replicate_spec expects a single walker")
     out = {}
     for key in ("m", "pos", "vel", "acc", "ei", "ej", "rest", "k", "c", "flags", "minl", "maxl", "stride", "mx",
-                "pinned", "charge", "radius"):
+                "pinned", "charge", "radius", "bounce_set"):
         if key in spec:
             a = np.asarray(spec[key])
             out[key] = np.tile(a, (n,) + (1,) * (a.ndim - 1))
@@ -154,7 +154,7 @@ def concat_specs(specs: List[dict]) -> dict:
     """Walkers of several flat CSR specs, in order, as one spec (offsets rebased)."""
     out = {}
     per = ("m", "pos", "vel", "acc", "ei", "ej", "rest", "k", "c", "flags", "minl", "maxl", "stride", "mx",
-           "pinned", "charge", "radius", "n_muscles")
+           "pinned", "charge", "radius", "bounce_set", "n_muscles")
     for key in per:
         parts = [np.asarray(s[key]) for s in specs if key in s]
         if len(parts) == len(specs):

@@ -502,6 +502,9 @@ def main():
     if in_world and not comm_eager and graph is None:
         # the same K steps again, now with RCCL's communicator up (the state has advanced; the work is the same):
         # the rate of a later rollout of an actor that gathers every rollout
+        if not do_gather:   # (--no-gather: no collective has run yet; one small all-reduce creates the communicator)
+            dist.all_reduce(torch.zeros(1, device=dev))
+            torch.cuda.synchronize()
         device_warm(stream, dev, warm_ms)
         if args.warmup > 0:
             env.run(acts_w, args.warmup, lanes=lanes)

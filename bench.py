@@ -499,7 +499,7 @@ def main():
                                "rollout's final observations gathered while these steps ran (inside the timed region)"}
 
     comm_live_max = None
-    if in_world and not comm_eager and graph is None:
+    if in_world and backend == "nccl" and not comm_eager and graph is None:
         # the same K steps again, now with RCCL's communicator up (the state has advanced; the work is the same):
         # the rate of a later rollout of an actor that gathers every rollout
         if not do_gather:   # (--no-gather: no collective has run yet; one small all-reduce creates the communicator)
@@ -640,7 +640,8 @@ def main():
                            "comm_live_value": round(world * N * args.steps / comm_live_max, 1),
                            "comm_live_note": "the same K steps timed again after the gather, communicator up, same "
                                              "warm-up (DESIGN §8)"} if comm_live_max is not None else
-                          {"comm": "RCCL's communicator created before the timed steps"} if in_world else {})},
+                          {"comm": ("RCCL's communicator created before the timed steps" if backend == "nccl" else
+                                    f"{backend} process group (rehearsal, no RCCL)")} if in_world else {})},
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,

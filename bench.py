@@ -246,6 +246,45 @@ def load_window(workload: str, walkers: int, lanes: int):
     return best
 
 
+class DistPlumbing:
+    """The timed region's process-group plumbing.  host_ctl (the RCCL default): the nccl group comes up without
+    device_id, so RCCL creates its communicator at the first collective that needs one (the rollout-end gather, after
+    the clock), and the barriers around the K steps and the max over ranks of their times go over a gloo group on the
+    host; otherwise (the pipelined gather, WG_COMM_EAGER=1, a gloo rehearsal) both use the default group, the nccl
+    one created with its communicator up front.  (tests/test_bench_dist.py runs both paths over gloo, world 2.)"""
+
+    def __init__(self, backend: str, dev, host_ctl: bool):
+        self.backend, self.dev, self.host_ctl, self.ctl = backend, dev, bool(host_ctl), None
+
+    def init(self) -> None:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if self.backend == "nccl" and not self.host_ctl:
+            dist.init_process_group("nccl", device_id=self.dev)
+        else:
+            dist.init_process_group(self.backend)
+        if self.host_ctl:
+            self.ctl = dist.new_group(backend="gloo")
+
+    def barrier(self) -> None:
+        import torch.distributed as dist
+        if self.ctl is not None:
+            dist.barrier(group=self.ctl)
+        else:
+            dist.barrier()
+
+    def max_over_ranks(self, vals):
+        import torch
+        import torch.distributed as dist
+        if self.ctl is not None:
+            t = torch.tensor(vals, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.ctl)
+        else:
+            t = torch.tensor(vals, dtype=torch.float64, device=self.dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return [float(x) for x in t.tolist()]
+
+
 def device_warm(stream, dev, ms: float) -> float:
     """Keep the GPU busy for `ms` with a VALU-bound kernel that is not a step (wg_launch_floor mode 2, on the bench
     stream), host-synchronised every few launches; returns the time spent (s)."""
@@ -334,34 +373,8 @@ def main():
     # exists run ~10 % slower in a K = 20 region and not in a K = 1,000 one; `timing.comm_live` times the
     # same K steps again after the gather, communicator up, so the line carries both.
     comm_eager = args.gather == "pipelined" or os.environ.get("WG_COMM_EAGER", "0") == "1"
-    ctl = None
-
-    def init_group():
-        nonlocal ctl
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if backend == "nccl":
-            if comm_eager:
-                dist.init_process_group("nccl", device_id=dev)
-            else:
-                dist.init_process_group("nccl")
-                ctl = dist.new_group(backend="gloo")
-        else:
-            dist.init_process_group(backend)
-
-    def barrier():
-        if ctl is not None:
-            dist.barrier(group=ctl)
-        else:
-            dist.barrier()
-
-    def max_over_ranks(vals):
-        if ctl is not None:
-            t = torch.tensor(vals, dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=ctl)
-        else:
-            t = torch.tensor(vals, dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return [float(x) for x in t.tolist()]
+    pg = DistPlumbing(backend, dev, host_ctl=(backend == "nccl" and not comm_eager))
+    init_group, barrier, max_over_ranks = pg.init, pg.barrier, pg.max_over_ranks
 
     # the process group comes up after the env's walker-range streams exist and have run the warm-up: RCCL's own
     # streams then cannot take the hardware queue a side stream would otherwise get (BatchedPhysicsEnv.__init__);

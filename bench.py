@@ -502,7 +502,8 @@ def main():
                        "gathered_bytes": int(world * sum(t.numel() * t.element_size() for t in sent.values())),
                        "ms": round(tg_ms, 4),
                        **({"first_gather_ms": round(first_gather_ms, 3),
-                           "first_gather_note": "the untimed gather before it: RCCL's communicator is created here"}
+                           "first_gather_note": ("the untimed gather before it: RCCL's communicator is created here"
+                                                 if backend == "nccl" else "the untimed gather before it")}
                           if first_gather_ms is not None else {}),
                        "value_incl_gather": round(world * N * args.steps / (wall_max + tg_ms * 1e-3), 1),
                        "note": "serial (default): this rollout's final observations [N, D] and its per-step reward "
@@ -609,8 +610,8 @@ def main():
                          "note": "step_loop: BatchedPhysicsEnv.step(policy(obs)) per env step (a full barrier per step: each "
                                  "launch drains alone); policy_loop: the walker ranges pipelined, each range's policy "
                                  "and step on its own stream (bit-identical trajectories, tests/test_gpu_policy_loop.py); "
-                                 "graph: the same loop captured as one HIP graph and replayed (HIP events around the "
-                                 "replay)"}
+                                 "graph: the same loop captured as one HIP graph per walker range, each replayed on its "
+                                 "own stream (HIP events around the replay)"}
         resident_ms = None
         if args.resident:
             env.run(acts_c, n1, lanes=1, resident=True)

@@ -118,21 +118,25 @@ class WalkerGraph:
         env._stale = self._stale
 
 
-class _PolicyGraph:
-    """policy_loop(graph=True): one captured graph per walker range and the stream it replays on; replay() forks the
-    ranges from the calling stream, replays each on its own stream and joins them back."""
+class _RangeGraphs:
+    """One captured graph per walker range and the stream it replays on (graph(), policy_loop(graph=True)): replay()
+    forks the ranges from the calling stream, replays each on its own stream and joins them back.  (One graph holding
+    the ranges as parallel branches replayed them serially on ROCm: 36.4 against 33.5 us per canonical step direct,
+    profiles/r05y_bench_graph.json.)"""
 
     def __init__(self, parts, cur):
         self.parts, self._cur = parts, cur
 
     def replay(self) -> None:
+        # range 0 replays on the calling stream itself (a single range needs no fork), the others on their own streams
         cur = torch.cuda.current_stream(self._cur.device)
-        for g, st in self.parts:
+        for g, st in self.parts[1:]:
             st.wait_stream(cur)
-        for g, st in self.parts:
+        for g, st in self.parts[1:]:
             with torch.cuda.stream(st):
                 g.replay()
-        for g, st in self.parts:
+        self.parts[0][0].replay()
+        for g, st in self.parts[1:]:
             cur.wait_stream(st)
 
 
@@ -444,7 +448,7 @@ class BatchedPhysicsEnv:
         return obs_out, reward_out, done_out
 
     def run(self, actions, n_steps: int, info: bool = True, lanes: Optional[int] = None, resident: bool = False,
-            record: Optional[dict] = None):
+            record: Optional[dict] = None, _only: Optional[int] = None):
         """Throughput path: n_steps env steps in one C call; step s acts with actions[s % T]
         ([T, N, A] device tensor; T == n_steps or 1) and overwrites obs/reward/done(/info) each step.  resident:
         wg_rollout (one launch for all steps where the batch allows it) instead of one launch per step.
@@ -456,15 +460,17 @@ class BatchedPhysicsEnv:
         record run env.reward / done / centroid / energy and the info extras are not this run's (they went to the
         record buffers, or were not computed): info() leaves those keys out until the next step() / observe() / run()
         without record."""
-        self.prepare_run(actions, n_steps, info=info, lanes=lanes, resident=resident, record=record)()
+        self.prepare_run(actions, n_steps, info=info, lanes=lanes, resident=resident, record=record, _only=_only)()
 
     def prepare_run(self, actions, n_steps: int, info: bool = True, lanes: Optional[int] = None,
-                    resident: bool = False, record: Optional[dict] = None) -> "PreparedRun":
+                    resident: bool = False, record: Optional[dict] = None,
+                    _only: Optional[int] = None) -> "PreparedRun":
         """run()'s argument checks, walker ranges and C structs, built once: the returned PreparedRun issues the same
         n_steps steps with ONE C call each time it is called (on the stream that was current here), so the host time
         between a caller's clock start and the first launch is one ctypes call (bench.py builds it before its timed
         region: ~35 us of Python before the first launch otherwise).  It holds raw pointers to `actions`,
-        the record buffers and the env's tensors: set_params / a reallocation of the outputs make it raise."""
+        the record buffers and the env's tensors: set_params / a reallocation of the outputs make it raise.
+        (_only = i, graph() only: walker range i alone, on the calling stream.)"""
         require_tensor(actions, "actions", self.device, torch.float32)
         if actions.dim() != 3:
             raise ValueError("actions must be a contiguous [n_steps or 1, N, A] device tensor")
@@ -504,14 +510,15 @@ class BatchedPhysicsEnv:
         n_steps = int(n_steps)
         if lanes > 1:
             capturing = torch.cuda.is_current_stream_capturing()
-            if entry == "wg_step" and not capturing and os.environ.get("WG_RANGE_ISSUE", "inter") != "seq":
+            if entry == "wg_step" and not capturing and _only is None and \
+                    os.environ.get("WG_RANGE_ISSUE", "inter") != "seq":
                 fn, args, keep = self._run_ranges_args(actions, n_steps, o, lanes)
                 if n_steps > 0:
                     for st in self._side[:lanes - 1]:
                         actions.record_stream(st)   # the allocator must not recycle it before the side streams are done
                 return PreparedRun(self, "wg_run_ranges", fn, args, keep, steps_valid, stale)
             # (range-by-range issue, a resident rollout over several ranges, or a graph capture: one C call per range)
-            return PreparedRun(self, entry, None, (actions, n_steps, o, lanes, entry), [o], steps_valid, stale,
+            return PreparedRun(self, entry, None, (actions, n_steps, o, lanes, entry, _only), [o], steps_valid, stale,
                                thunk=self._run_lanes)
         # (a resident launch writes the steps output only where the resident kernel runs: uniform batches, which
         # have no steps_out)
@@ -600,13 +607,14 @@ class BatchedPhysicsEnv:
                 n_steps, self._range_events(lanes))
         return _lib.load().wg_run_ranges, args, keep
 
-    def _run_lanes(self, actions, n_steps: int, o_full, lanes: int, entry: str = "wg_step"):
+    def _run_lanes(self, actions, n_steps: int, o_full, lanes: int, entry: str = "wg_step", only: Optional[int] = None):
         """n_steps with the walkers split into `lanes` contiguous ranges, each stepped by its own stream, one C call
         per range (the range-by-range form; prepare_run issues the ranges step by step through wg_run_ranges): the
         ranges are independent, so one range's step t + 1 fills the GPU while another's step t drains (the
         launch tail).  Every walker still takes every step, one launch per step per range; the calling
         stream waits for all ranges before returning (stream-ordered, no host sync).  o_full: the whole batch's
-        WgOutputs (a uniform range's are its pointers advanced to the range's first walker)."""
+        WgOutputs (a uniform range's are its pointers advanced to the range's first walker).  only = i: range i
+        alone, on the calling stream (graph() captures one graph per range)."""
         T, n, cols = actions.shape
         cur = torch.cuda.current_stream(self.device)
         self.reserve_streams(lanes)
@@ -615,12 +623,13 @@ class BatchedPhysicsEnv:
         bounds = self._range_bounds(lanes)
         capturing = torch.cuda.is_current_stream_capturing()
         start = torch.cuda.Event()
-        start.record(cur)
+        if only is None:
+            start.record(cur)
         done = []
-        for i in range(lanes):
+        for i in (range(lanes) if only is None else [only]):
             w0, w1 = bounds[i], bounds[i + 1]
-            st = cur if i == 0 else self._side[i - 1]
-            if i:
+            st = cur if (i == 0 or only is not None) else self._side[i - 1]
+            if st is not cur:
                 st.wait_event(start)
             if ragged:
                 sub, o, act = self.batch.struct, o_full, C.c_void_p(actions.data_ptr())
@@ -631,7 +640,7 @@ class BatchedPhysicsEnv:
             _lib.check(getattr(L, entry)(C.byref(sub), C.byref(self._pstruct), act, cols, cols,
                                          0 if T == 1 else self.N * cols, C.byref(o), n_steps, plan, nblk,
                                          C.c_void_p(st.cuda_stream)), entry)
-            if i:
+            if st is not cur:
                 if not capturing:
                     actions.record_stream(st)   # the allocator must not recycle it before the side stream is done
                 ev = torch.cuda.Event()
@@ -788,7 +797,7 @@ class BatchedPhysicsEnv:
                     body(st, only=r)
             cur.wait_stream(st)
             parts.append((g, st))
-        self._policy_graph = _PolicyGraph(parts, cur)   # (kept until the next call: the replay may still be running)
+        self._policy_graph = _RangeGraphs(parts, cur)   # (kept until the next call: the replay may still be running)
         self._policy_graph.replay()
 
     def _caller_bounds(self, lanes: int):
@@ -817,20 +826,25 @@ class BatchedPhysicsEnv:
 
     def graph(self, actions, n_steps: int, info: bool = True, lanes: Optional[int] = None):
         """Capture run(actions, n_steps) into a HIP graph (torch.cuda.CUDAGraph over the ROCm runtime) and
-        return it as a WalkerGraph; replay() then advances the batch n_steps with one host call, the two walker
-        ranges' streams forked and joined inside the graph.  `actions` is kept alive by the WalkerGraph (and may be
+        return it as a WalkerGraph; replay() then advances the batch n_steps with one host call: one graph per walker
+        range, each replayed on its own stream, forked from and joined back to the calling stream (_RangeGraphs).  `actions` is kept alive by the WalkerGraph (and may be
         refilled in place); the graph reads the batch and output tensors this env owns and the parameters as
         captured, so set_params() (or any reallocation of the outputs) makes replay() raise."""
-        g = torch.cuda.CUDAGraph()
-        side = torch.cuda.Stream(device=self.device)
-        side.wait_stream(torch.cuda.current_stream(self.device))
+        lanes = self._lanes(lanes)
+        cur = torch.cuda.current_stream(self.device)
         steps_at, stale = self._steps_at, self._stale   # capture runs nothing: the outputs' validity is unchanged
-        with torch.cuda.stream(side):           # capture off the default stream, as torch requires
-            with torch.cuda.graph(g, stream=side):
-                self.run(actions, n_steps, info=info, lanes=lanes)
-        torch.cuda.current_stream(self.device).wait_stream(side)
+        parts = []
+        for r in range(lanes):   # one graph per walker range, each replayed on a stream of its own (_RangeGraphs)
+            g = torch.cuda.CUDAGraph()
+            side = torch.cuda.Stream(device=self.device)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):           # capture off the default stream, as torch requires
+                with torch.cuda.graph(g, stream=side):
+                    self.run(actions, n_steps, info=info, lanes=lanes, _only=r if lanes > 1 else None)
+            cur.wait_stream(side)
+            parts.append((g, side))
         self._steps_at, self._stale = steps_at, stale
-        return WalkerGraph(self, g, actions, info=info)
+        return WalkerGraph(self, _RangeGraphs(parts, cur), actions, info=info)
 
     def observe(self):
         o = self._outputs(self.obs, self.reward, self.done, self.centroid, self.energy, steps=self.steps_out,

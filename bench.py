@@ -586,6 +586,23 @@ def main():
             e1.record(stream)
             torch.cuda.synchronize()
             ranges_ms = e0.elapsed_time(e1) / n1
+            # the loop's own cost: the same policy_loop with a policy that launches nothing (preallocated actions of
+            # each range's row count), so the difference to the open loop is the loop's host issue and per-range checks
+            null_acts = {}
+
+            def pol_null(rows, t):
+                a = null_acts.get(rows.shape[0])
+                if a is None:
+                    a = null_acts[rows.shape[0]] = torch.zeros((rows.shape[0], Acols), device=dev)
+                return a
+            env.policy_loop(pol_null, 5, lanes=lanes)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            env.policy_loop(pol_null, n1, lanes=lanes)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            null_ms = e0.elapsed_time(e1) / n1
             env.policy_loop(pol, 5, lanes=lanes, graph=True)    # warm the capture path
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -606,12 +623,14 @@ def main():
                          "step_loop_ms_per_step": round(step_pol_ms, 5),
                          "policy_loop_ms_per_step": round(ranges_ms, 5),
                          "policy_loop_graph_ms_per_step": round(ranges_graph_ms, 5),
+                         "policy_loop_null_policy_ms_per_step": round(null_ms, 5),
                          "lanes": lanes,
                          "note": "step_loop: BatchedPhysicsEnv.step(policy(obs)) per env step (a full barrier per step: each "
                                  "launch drains alone); policy_loop: the walker ranges pipelined, each range's policy "
                                  "and step on its own stream (bit-identical trajectories, tests/test_gpu_policy_loop.py); "
                                  "graph: the same loop captured as one HIP graph per walker range, each replayed on its "
-                                 "own stream (HIP events around the replay)"}
+                                 "own stream (HIP events around the replay); null_policy: policy_loop with a policy that "
+                                 "launches nothing (the loop's own cost against the open loop)"}
         resident_ms = None
         if args.resident:
             env.run(acts_c, n1, lanes=1, resident=True)

@@ -528,15 +528,18 @@ def test_run_lanes_bit_identical(monkeypatch):
     assert all(torch.equal(a, b) for a, b in zip(*outs))
 
 
-def test_graph_replay_equals_run():
-    """run() captured into a HIP graph (both walker ranges' streams inside it) and replayed gives the same
-    bits as the direct calls."""
+@pytest.mark.parametrize("kind", ["canonical", "ragged"])
+def test_graph_replay_equals_run(kind):
+    """run() captured as HIP graphs (one per walker range, each replayed on its own stream) and replayed gives the
+    same bits as the direct calls, uniform and ragged (plan slices) batches."""
     import torch
     from walker_gym_amd.batched_env import BatchedPhysicsEnv
-    from walker_gym_amd.synthetic import canonical_walkers
+    from walker_gym_amd.synthetic import canonical_walkers, ragged_walkers
     N = 12000
-    env = BatchedPhysicsEnv(canonical_walkers(N, seed=6), device="cuda:0", in3d=1)
-    acts = (torch.rand((10, N, 8), generator=torch.Generator(device="cuda:0").manual_seed(6), device="cuda:0")
+    spec = canonical_walkers(N, seed=6) if kind == "canonical" else ragged_walkers(N, seed=6, mmin=4, mmax=32)
+    env = BatchedPhysicsEnv(spec, device="cuda:0", in3d=1)
+    A = env.batch.A
+    acts = (torch.rand((10, N, A), generator=torch.Generator(device="cuda:0").manual_seed(6), device="cuda:0")
             * 2 - 1).contiguous()
     sd0 = env.batch.state_dict()
     env.run(acts, 10, lanes=1)
@@ -553,6 +556,7 @@ def test_graph_replay_equals_run():
     torch.cuda.synchronize()
     got = [t.clone() for t in env.batch.state_dict().values()] + [env.obs.clone(), env.energy.clone()]
     assert all(torch.equal(a, b) for a, b in zip(ref, got))
+    assert torch.equal(env.info()["steps"], torch.full((N,), 20, dtype=torch.int32, device="cuda:0"))
     # the graph holds the parameters and buffers as captured: after set_params it refuses to replay
     env.set_params(dampk=0.5)
     with pytest.raises(RuntimeError, match="stale"):

@@ -45,11 +45,20 @@ def main():
     spec = canonical_walkers(N, seed=1000)
     mx, _ = max_degree(spec, N, M, K)
     order = np.argsort(mx, kind="stable")
+    # descending: the tiles with the longest mass loops first, the shortest last (longest-processing-time-first
+    # order against the launch's drain)
+    order_d = order[::-1].copy()
+    # lpt: descending within each XCD's contiguous chunk of tiles (xcd_block gives XCD x the x-th eighth of the tiles,
+    # dispatched in order), the walkers dealt round-robin so every chunk has the same degree mix
+    order_l = np.concatenate([order_d[j::8] for j in range(8)])
     sspec = permute(spec, order, N, M, K, A)
+    dspec = permute(spec, order_l, N, M, K, A)
     wave_max = {"generated": float(mx.reshape(-1, 4).max(axis=1).mean()),
-                "sorted": float(mx[order].reshape(-1, 4).max(axis=1).mean())}
+                "sorted": float(mx[order].reshape(-1, 4).max(axis=1).mean()),
+                "sorted_lpt": float(mx[order_l].reshape(-1, 4).max(axis=1).mean())}
     envs = {"generated": BatchedPhysicsEnv(spec, device="cuda:0", in3d=1),
-            "sorted": BatchedPhysicsEnv(sspec, device="cuda:0", in3d=1)}
+            "sorted": BatchedPhysicsEnv(sspec, device="cuda:0", in3d=1),
+            "sorted_lpt": BatchedPhysicsEnv(dspec, device="cuda:0", in3d=1)}
     acts = (torch.rand((steps, N, A), device="cuda:0") * 2 - 1).contiguous()
     res = {k: {"lanes1": [], "lanes2": []} for k in envs}
     for r in range(rounds):

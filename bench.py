@@ -306,6 +306,30 @@ def device_warm(stream, dev, ms: float) -> float:
     return time.perf_counter() - t0
 
 
+def device_busy(stream, dev, launches: int) -> None:
+    """Enqueue `launches` of the warm-up kernel (wg_launch_floor mode 2, ~0.1 ms each) without waiting: the GPU stays
+    busy while the host waits in the barrier that opens the timed region, so the steps start at the clocks of a busy
+    GPU as they do without a process group (an idle gap of a barrier's length before the clock otherwise)."""
+    import ctypes as C
+    import torch
+    from walker_gym_amd import _lib
+    blocks, threads = 4096, 256
+    src = torch.zeros(blocks * threads, device=dev)
+    dst = torch.empty_like(src)
+    _lib.check(_lib.load().wg_launch_floor(2, blocks, threads, C.c_void_p(src.data_ptr()), C.c_void_p(dst.data_ptr()),
+                                           int(launches), C.c_void_p(stream.cuda_stream)), "wg_launch_floor")
+    src.record_stream(stream)
+    dst.record_stream(stream)
+
+
+def host_spin(us: float) -> None:
+    """Busy-wait `us` microseconds on the host: after a barrier that slept in a socket wait, the core is brought back to
+    speed before the clock starts (the launch issue of the first steps runs on it)."""
+    t = time.perf_counter()
+    while time.perf_counter() - t < us * 1e-6:
+        pass
+
+
 def timed(env, acts, steps, lanes, stream):
     """Per-step kernel time with HIP events on `stream` (the calling stream waits for every walker range)."""
     import torch
@@ -439,7 +463,10 @@ def main():
     prep = env.prepare_run(acts, args.steps, lanes=lanes, record=rec) if graph is None else None
     torch.cuda.synchronize()
     if in_world:
+        if os.environ.get("WG_BENCH_BARRIER_BUSY", "1") != "0":
+            device_busy(stream, dev, 3)   # (the synchronize below waits for it: the clock starts after)
         barrier()
+        host_spin(float(os.environ.get("WG_BENCH_SPIN_US", "300")))
     prev_obs = env.obs.clone() if do_gather and args.gather == "pipelined" else None
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -523,7 +550,10 @@ def main():
         if args.warmup > 0:
             env.run(acts_w, args.warmup, lanes=lanes)
         torch.cuda.synchronize()
+        if os.environ.get("WG_BENCH_BARRIER_BUSY", "1") != "0":
+            device_busy(stream, dev, 3)
         barrier()
+        host_spin(float(os.environ.get("WG_BENCH_SPIN_US", "300")))
         torch.cuda.synchronize()
         tl = time.perf_counter()
         prep()

@@ -13,10 +13,12 @@ with obs/reward/done/info materialised every step.  The batch is split into walk
 HIP streams (BatchedPhysicsEnv.run lanes: 2 for batches of >= 2^19 masses), one launch per range per step:
 every walker takes every step, and one range's next step fills the GPU while the other's drains.  Inputs
 (state, topology and a distinct U(-1,1) action tensor for every timed step) are resident in HBM before timing.
-Weak scaling: each rank owns its own `--walkers` walkers (no data-path collective); one rollout-end gather of a
-rollout's final observations (one RCCL all_gather_into_tensor) runs inside the timed region: by default this rollout's,
-after its last step (`--gather serial`), or the previous rollout's while this one steps (`--gather pipelined`,
-double-buffered as an actor loop would run it; slower on one MI355X).
+Weak scaling: each rank owns its own `--walkers` walkers (no data-path collective).  Inside a torch.distributed world
+the rollout-end gather (RCCL all_gather_into_tensor of the final observations and the per-step reward / done records)
+runs after the barrier that closes the K timed steps (`--gather serial`, the default): `value` is the K steps,
+`value_incl_gather` the steps and the gather; RCCL's communicator is created by an untimed first gather, after the
+clock, and the barriers and the max over ranks go over a gloo group (DistPlumbing).  `--gather pipelined` gathers the
+previous rollout's observations while this one steps, inside the timed region (slower on one MI355X).
 Rank 0 prints ONE JSON line.  Workloads: canonical (M=16, K=40, A=8; config 3/4),
 balance (Balance-v0; config 2 at --walkers 4096), ragged (M ~ U{4..32}; config 5), chain (performance_demo's
 chain of --chain-points masses with per-walker Point.gravity; §8(f) 3).

@@ -528,8 +528,8 @@ def test_run_lanes_bit_identical(monkeypatch):
     assert all(torch.equal(a, b) for a, b in zip(*outs))
 
 
-@pytest.mark.parametrize("kind", ["canonical", "ragged"])
-def test_graph_replay_equals_run(kind):
+@pytest.mark.parametrize("kind,lanes", [("canonical", 2), ("ragged", 2), ("canonical", 3), ("ragged", 1)])
+def test_graph_replay_equals_run(kind, lanes):
     """run() captured as HIP graphs (one per walker range, each replayed on its own stream) and replayed gives the
     same bits as the direct calls, uniform and ragged (plan slices) batches."""
     import torch
@@ -548,7 +548,7 @@ def test_graph_replay_equals_run(kind):
     ref = [t.clone() for t in env.batch.state_dict().values()] + [env.obs.clone(), env.energy.clone()]
     env.batch.load_state_dict(sd0)
     torch.cuda.synchronize()
-    g = env.graph(acts, 10, lanes=2)   # capture records the launches (two streams) without running them
+    g = env.graph(acts, 10, lanes=lanes)   # capture records the launches (one graph per range) without running them
     env.batch.load_state_dict(sd0)
     torch.cuda.synchronize()
     g.replay()

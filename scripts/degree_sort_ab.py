@@ -51,14 +51,20 @@ def main():
     # lpt: descending within each XCD's contiguous chunk of tiles (xcd_block gives XCD x the x-th eighth of the tiles,
     # dispatched in order), the walkers dealt round-robin so every chunk has the same degree mix
     order_l = np.concatenate([order_d[j::8] for j in range(8)])
+    # lpt2: the same per XCD chunk of each of the two walker ranges (16 chunks: range r's launch gives XCD x its x-th
+    # eighth), for the two-range step
+    order_l2 = np.concatenate([order_d[j::16] for j in range(16)])
     sspec = permute(spec, order, N, M, K, A)
     dspec = permute(spec, order_l, N, M, K, A)
+    d2spec = permute(spec, order_l2, N, M, K, A)
     wave_max = {"generated": float(mx.reshape(-1, 4).max(axis=1).mean()),
                 "sorted": float(mx[order].reshape(-1, 4).max(axis=1).mean()),
-                "sorted_lpt": float(mx[order_l].reshape(-1, 4).max(axis=1).mean())}
+                "sorted_lpt": float(mx[order_l].reshape(-1, 4).max(axis=1).mean()),
+                "sorted_lpt2": float(mx[order_l2].reshape(-1, 4).max(axis=1).mean())}
     envs = {"generated": BatchedPhysicsEnv(spec, device="cuda:0", in3d=1),
             "sorted": BatchedPhysicsEnv(sspec, device="cuda:0", in3d=1),
-            "sorted_lpt": BatchedPhysicsEnv(dspec, device="cuda:0", in3d=1)}
+            "sorted_lpt": BatchedPhysicsEnv(dspec, device="cuda:0", in3d=1),
+            "sorted_lpt2": BatchedPhysicsEnv(d2spec, device="cuda:0", in3d=1)}
     acts = (torch.rand((steps, N, A), device="cuda:0") * 2 - 1).contiguous()
     res = {k: {"lanes1": [], "lanes2": []} for k in envs}
     for r in range(rounds):

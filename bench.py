@@ -14,11 +14,14 @@ HIP streams (BatchedPhysicsEnv.run lanes: 2 for batches of >= 2^19 masses), one 
 every walker takes every step, and one range's next step fills the GPU while the other's drains.  Inputs
 (state, topology and a distinct U(-1,1) action tensor for every timed step) are resident in HBM before timing.
 Weak scaling: each rank owns its own `--walkers` walkers (no data-path collective).  Inside a torch.distributed world
+RCCL's communicator is created before the env's warm-up and checked (`comm`: its size by an all_reduce of ones, every
+rank's device and PCI address distinct), the job time is max(t1) - min(t0) over ranks on the node's shared clock, and
 the rollout-end gather (RCCL all_gather_into_tensor of the final observations and the per-step reward / done records)
 runs after the barrier that closes the K timed steps (`--gather serial`, the default): `value` is the K steps,
-`value_incl_gather` the steps and the gather; RCCL's communicator is created by an untimed first gather, after the
-clock, and the barriers and the max over ranks go over a gloo group (DistPlumbing).  `--gather pipelined` gathers the
-previous rollout's observations while this one steps, inside the timed region (slower on one MI355X).
+`value_incl_gather` the steps and the gather, and `gather.content_check` compares every rank's checksums of what it
+sent with its shard of the gathered tensors (a failed check exits 3).  `--gather pipelined` gathers the previous
+rollout's observations while this one steps, inside the timed region (slower on one MI355X).
+After the K steps `sustained` times 1,000 steps and a ~2 s run of the same walker ranges (the long-run clock).
 Rank 0 prints ONE JSON line.  Workloads: canonical (M=16, K=40, A=8; config 3/4),
 balance (Balance-v0; config 2 at --walkers 4096), ragged (M ~ U{4..32}; config 5), chain (performance_demo's
 chain of --chain-points masses with per-walker Point.gravity; §8(f) 3).
@@ -79,6 +82,10 @@ def parse(argv=None):
                          "final observations, after its last step) or pipelined (the previous rollout's, gathered "
                          "while this rollout steps; measured slower on one MI355X: RCCL's kernels stall the steps)")
     ap.add_argument("--no-control", action="store_true", help="skip the single-launch (lanes 1) control timing")
+    ap.add_argument("--sustained-steps", type=int, default=1000,
+                    help="after the K timed steps: time this many steps (SURVEY §8(d)'s 1,000) and then the same "
+                         "prepared run repeated for --sustained-seconds, reported as `sustained` (0: skip)")
+    ap.add_argument("--sustained-seconds", type=float, default=2.0)
     ap.add_argument("--dry-run", action="store_true", help="rank plumbing only (no GPU): every rank reports itself")
     ap.add_argument("--device-warm-ms", type=float, default=None,
                     help="ms of a VALU-bound non-step kernel (wg_launch_floor mode 2) right before the W warm-up steps "
@@ -233,58 +240,87 @@ def load_traffic(workload: str, walkers: int):
     return best
 
 
-def load_window(workload: str, walkers: int, lanes: int):
-    """The rocprofv3 per-step time of the multi-range timed region (scripts/trace_kernels.py --window: the span of the
-    region's launches by their own timestamps) from a committed record (profiles/*window*.json), if present."""
-    import glob
-    best = None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*window*.json"))):
-        try:
-            d = json.load(open(f))
-        except Exception:
-            continue
-        if d.get("workload") == workload and d.get("walkers") == walkers and d.get("lanes") == lanes:
-            best = dict(d, file=os.path.relpath(f, ROOT))
-    return best
+def clock() -> float:
+    """Host CLOCK_MONOTONIC in seconds: one clock for every process of the node, so the ranks' start and end times
+    compare directly (the job's span is max over ranks of t1 - min over ranks of t0)."""
+    return time.clock_gettime(time.CLOCK_MONOTONIC)
 
 
 class DistPlumbing:
-    """The timed region's process-group plumbing.  host_ctl (the RCCL default): the nccl group comes up without
-    device_id, so RCCL creates its communicator at the first collective that needs one (the rollout-end gather, after
-    the clock), and the barriers around the K steps and the max over ranks of their times go over a gloo group on the
-    host; otherwise (the pipelined gather, WG_COMM_EAGER=1, a gloo rehearsal) both use the default group, the nccl
-    one created with its communicator up front.  (tests/test_bench_dist.py runs both paths over gloo, world 2.)"""
+    """The process groups of a run inside a torch.distributed world.  The default group carries the data path's
+    backend: nccl (= RCCL), created with device_id so that RCCL's communicator is up before any timed region (the
+    steady state of an actor that gathers every rollout), or gloo to rehearse ranks.  With nccl a second,
+    gloo group carries the host-side plumbing: the barriers that open and close timed regions, the exchange of the
+    ranks' clocks and identities, and the gathered-rollout checksums.  (tests/test_bench_dist.py runs it over gloo at
+    world 2 and world 8.)"""
 
-    def __init__(self, backend: str, dev, host_ctl: bool):
-        self.backend, self.dev, self.host_ctl, self.ctl = backend, dev, bool(host_ctl), None
+    def __init__(self, backend: str, dev):
+        self.backend, self.dev, self.ctl = backend, dev, None
 
     def init(self) -> None:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if self.backend == "nccl" and not self.host_ctl:
+        if self.backend == "nccl":
             dist.init_process_group("nccl", device_id=self.dev)
+            self.ctl = dist.new_group(backend="gloo")
         else:
             dist.init_process_group(self.backend)
-        if self.host_ctl:
-            self.ctl = dist.new_group(backend="gloo")
+
+    @property
+    def host_group(self):
+        """The gloo group for CPU tensors (None: the default group, itself gloo)."""
+        return self.ctl
 
     def barrier(self) -> None:
         import torch.distributed as dist
-        if self.ctl is not None:
-            dist.barrier(group=self.ctl)
-        else:
-            dist.barrier()
+        dist.barrier(group=self.ctl)
 
     def max_over_ranks(self, vals):
         import torch
         import torch.distributed as dist
-        if self.ctl is not None:
-            t = torch.tensor(vals, dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.ctl)
-        else:
-            t = torch.tensor(vals, dtype=torch.float64, device=self.dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t = torch.tensor(vals, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.ctl)
         return [float(x) for x in t.tolist()]
+
+    def span(self, t0: float, t1: float) -> tuple:
+        """(max over ranks of t1 - min over ranks of t0, max over ranks of t1 - t0): the job's time from the first rank's
+        start to the last rank's end on the shared clock (start skew included), and the slowest rank's own time."""
+        a, b, c = self.max_over_ranks([t1, -t0, t1 - t0])
+        return a + b, c
+
+    def comm_size(self) -> int:
+        """A one-element all_reduce of ones on the default group (RCCL's communicator with nccl): the sum is the number
+        of ranks the communicator actually spans."""
+        import torch
+        import torch.distributed as dist
+        dv = self.dev if self.backend == "nccl" else torch.device("cpu")
+        t = torch.ones(1, dtype=torch.float32, device=dv)
+        dist.all_reduce(t)
+        return int(round(float(t.item())))
+
+    def all_objects(self, obj) -> list:
+        import torch.distributed as dist
+        out = [None] * dist.get_world_size()
+        dist.all_gather_object(out, obj, group=self.ctl)
+        return out
+
+
+def comm_report(pg: "DistPlumbing", world: int, identity: dict, strict: bool) -> dict:
+    """The line's `comm` block: the communicator's size (must equal the world), every rank's device
+    and PCI address (must be distinct when strict, i.e. RCCL; a gloo rehearsal may share one GPU).  A failed check ends
+    the run with exit status 3 on every rank."""
+    size = pg.comm_size()
+    ids = pg.all_objects(identity)
+    from walker_gym_amd.distributed import check_distinct
+    distinct, why = check_distinct(ids)
+    ok = size == world and (distinct or not strict)
+    rep = {"backend": pg.backend, "communicator_size": size, "world": world, "ranks": ids, "distinct_devices": distinct,
+           "ok": ok}
+    if not ok:
+        msg = f"communicator spans {size} ranks, world {world}" if size != world else why
+        print(f"bench.py: comm check failed: {msg}", file=sys.stderr, flush=True)
+        sys.exit(3)
+    return rep
 
 
 def device_warm(stream, dev, ms: float) -> float:
@@ -377,7 +413,7 @@ def main():
     import torch
     import torch.distributed as dist
     from walker_gym_amd.batched_env import BatchedPhysicsEnv
-    from walker_gym_amd.distributed import gather_rollout, gather_rollout_async
+    from walker_gym_amd.distributed import gather_rollout, gather_rollout_async, rank_identity, verify_gathered
     from walker_gym_amd.layout import layout_bytes_per_walker_step
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -386,28 +422,28 @@ def main():
     backend = os.environ.get("WG_DIST_BACKEND", "nccl")   # nccl = RCCL; gloo only to rehearse ranks on one GPU
     if backend != "nccl":
         local = local % max(1, torch.cuda.device_count())
-    # inside a torch.distributed world (WORLD_SIZE set by torch.distributed.run), world 1 included: the process
-    # group and the rollout-end gather run at every N, so `torchrun --nproc-per-node 1 bench.py` executes exactly
-    # the code of the 8-GPU run (RCCL init, barriers, max-over-ranks wall time, all_gather_into_tensor)
+    # inside a torch.distributed world (WORLD_SIZE set by torch.distributed.run), world 1 included: the process group,
+    # its checks and the rollout-end gather run at every N, so `torchrun --nproc-per-node 1 bench.py` executes exactly
+    # the code of the 8-GPU run (RCCL init, barriers, job span over ranks, all_gather_into_tensor)
     in_world = "WORLD_SIZE" in os.environ
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    pg = DistPlumbing(backend, dev) if in_world else None
+    comm = None
 
-    # RCCL's communicator is created by the first collective that needs it: the rollout-end gather, after the clock
-    # (the pipelined gather, which runs inside the timed region, and WG_COMM_EAGER=1 create it up front).  The timed
-    # region's barriers and the max over ranks go over a gloo group on the host.  Steps issued while a communicator
-    # exists run ~10 % slower in a K = 20 region and not in a K = 1,000 one; `timing.comm_live` times the
-    # same K steps again after the gather, communicator up, so the line carries both.
-    comm_eager = args.gather == "pipelined" or os.environ.get("WG_COMM_EAGER", "0") == "1"
-    pg = DistPlumbing(backend, dev, host_ctl=(backend == "nccl" and not comm_eager))
-    init_group, barrier, max_over_ranks = pg.init, pg.barrier, pg.max_over_ranks
+    def bring_up():
+        # RCCL's communicator comes up here, before any timed region (the steady state of an actor that
+        # gathers every rollout; the timed steps of round 5 ran before it existed), and proves its size and devices
+        nonlocal comm
+        pg.init()
+        comm = comm_report(pg, world, dict(rank=rank, local_rank=local, **rank_identity(dev)), strict=backend == "nccl")
 
-    # the process group comes up after the env's walker-range streams exist and have run the warm-up: RCCL's own
-    # streams then cannot take the hardware queue a side stream would otherwise get (BatchedPhysicsEnv.__init__);
+    # the process group comes up after the env's walker-range streams exist and have run a step: RCCL's own streams
+    # then cannot take the hardware queue a side stream would otherwise get (BatchedPhysicsEnv.__init__);
     # WG_DIST_INIT_FIRST=1 (diagnostic) restores the other order
     dist_first = os.environ.get("WG_DIST_INIT_FIRST", "0") == "1"
     if in_world and dist_first:
-        init_group()
+        bring_up()
 
     N = args.walkers
     spec, params = make_spec(args.workload, N, seed=1000 + rank, chain_points=args.chain_points)
@@ -423,37 +459,33 @@ def main():
 
     graph = env.graph(acts, args.steps, lanes=lanes) if args.graph else None
     if in_world and not dist_first:
-        # one step on the walker ranges' streams binds their hardware queues before RCCL creates its own streams; the
-        # W warm-up steps then run after the group is up, right before the timed region: the group's initialisation
-        # leaves the GPU idle for ~1-3 s, and steps timed straight after that idle ran ~25 % slow for their first
-        # ~2 ms (torchrun world 1, K = 20: 47.5-49.6 us per step by events against 37.7 with gloo, whose group comes
-        # up in 4 ms; profiles/r04o_*, r04r_*)
+        # one step on the walker ranges' streams binds their hardware queues before RCCL creates its own streams
         env.run(acts_w[:1], 1, lanes=lanes)
         torch.cuda.synchronize()
-        init_group()
+        bring_up()
     do_gather = in_world and not args.no_gather
-    # pipelined gather: the send buffer holds the previous rollout's final observations (here the warm-up's)
     # the rollout SURVEY §8(e) gathers: every step's reward and done flags (written by the steps at per-step offsets,
     # the same bytes as overwriting one row) and the final observations
     rec = None
     dst = 0 if args.gather_to == "root" else None
-
-    def warm_gather():
-        # one untimed gather of the same tensors, so that the timed one is RCCL's steady state (its first all-gather
-        # of a shape sets up buffers: 0.68 ms against 0.16-0.25 warm at world 1, profiles/r04t_nccl1); the first
-        # collective also creates the communicator
-        gather_rollout(env.obs, n_total=world * N, dst=dst)
-        if rec is not None:
-            gather_rollout(rec["reward"], n_total=world * N, dim=1, dst=dst)
-            gather_rollout(rec["done"], n_total=world * N, dim=1, dst=dst)
-
     if do_gather and graph is None and args.gather != "pipelined":
         rec = {"reward": torch.empty((args.steps, N), dtype=torch.float32, device=dev),
                "done": torch.empty((args.steps, N), dtype=torch.uint8, device=dev),
                "energy": torch.empty((args.steps, N), dtype=torch.float32, device=dev),
                "centroid": torch.empty((args.steps, N, 3), dtype=torch.float32, device=dev)}
-    if do_gather and comm_eager:
-        warm_gather()
+
+    def gather_all(obs):
+        out = {"obs": gather_rollout(obs, n_total=world * N, dst=dst)}
+        if rec is not None:
+            out["reward"] = gather_rollout(rec["reward"], n_total=world * N, dim=1, dst=dst)
+            out["done"] = gather_rollout(rec["done"], n_total=world * N, dim=1, dst=dst)
+        return out
+
+    if do_gather:
+        # one untimed gather of the same tensors, so that the timed one is RCCL's steady state (its first all-gather of
+        # a shape sets up buffers: 0.68 ms against 0.16-0.25 warm at world 1, profiles/r04t_nccl1)
+        gather_all(env.obs)
+        torch.cuda.synchronize()
     warm_ms = args.device_warm_ms if args.device_warm_ms is not None else float(os.environ.get("WG_BENCH_WARM_MS", "100"))
     warm_s = device_warm(stream, dev, warm_ms)
     if args.warmup > 0:
@@ -461,18 +493,37 @@ def main():
     if graph is not None:
         graph.replay()                         # warm the graph path too
     # the timed call's arguments, walker ranges and C structs built here: inside the timed region the K steps are one
-    # C call (run() spends ~35 us of Python before its first launch, which the GPU would idle through; DESIGN §7)
+    # C call (run() spends ~35 us of Python before its first launch, which the GPU would idle through; DESIGN §6)
     prep = env.prepare_run(acts, args.steps, lanes=lanes, record=rec) if graph is None else None
     torch.cuda.synchronize()
-    if in_world:
-        if os.environ.get("WG_BENCH_BARRIER_BUSY", "1") != "0":
-            device_busy(stream, dev, 3)   # (the synchronize below waits for it: the clock starts after)
-        barrier()
-        host_spin(float(os.environ.get("WG_BENCH_SPIN_US", "300")))
+
+    def open_region() -> float:
+        # every rank: the GPU kept busy through the opening barrier (three launches of the warm-up kernel, waited for
+        # below) and the host core awake after it, then synchronize; t0
+        if in_world:
+            if os.environ.get("WG_BENCH_BARRIER_BUSY", "1") != "0":
+                device_busy(stream, dev, 3)
+            pg.barrier()
+            host_spin(float(os.environ.get("WG_BENCH_SPIN_US", "300")))
+        torch.cuda.synchronize()
+        return clock()
+
+    def close_region(t0: float) -> tuple:
+        # t1 after this rank's synchronize; the job's time = max(t1) - min(t0) over ranks on the node's shared clock,
+        # then the closing barrier (its cost stays beside the figure)
+        torch.cuda.synchronize()
+        t1 = clock()
+        if not in_world:
+            return t1 - t0, t1 - t0, t1 - t0
+        job, slowest = pg.span(t0, t1)
+        pg.barrier()
+        torch.cuda.synchronize()
+        return job, slowest, pg.max_over_ranks([clock() - t0])[0]
+
     prev_obs = env.obs.clone() if do_gather and args.gather == "pipelined" else None
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
+    t0 = open_region()
     ev0.record(stream)
     pending = None
     if prev_obs is not None:
@@ -486,85 +537,96 @@ def main():
     gathered = None
     if pending is not None:
         gathered = {"obs": pending.wait()}
-    torch.cuda.synchronize()
-    # each rank's clock stops once its own K steps are done (t0 came after the opening barrier and synchronize, so the
-    # ranks start together); the MAX over ranks is the job's time.  The closing barrier follows, off the clock: an RCCL
-    # barrier is an all-reduce whose launch and host wait cost ~50-100 us, 7-15 % of a 20-step region at world 1
-    # (profiles/r05a_*), which the max over ranks already accounts for
-    wall = time.perf_counter() - t0
-    if in_world:
-        barrier()
-    torch.cuda.synchronize()
-    wall_bar = time.perf_counter() - t0
+    wall_max, slowest_rank, wall_bar_max = close_region(t0)
     step_ms = ev0.elapsed_time(ev1) / args.steps
 
-    wall_max, wall_bar_max = max_over_ranks([wall, wall_bar]) if in_world else (wall, wall_bar)
     gather_info = None
-    first_gather_ms = None
-    if do_gather and not comm_eager:
-        torch.cuda.synchronize()
-        tf = time.perf_counter()
-        warm_gather()
-        torch.cuda.synchronize()
-        first_gather_ms = max_over_ranks([time.perf_counter() - tf])[0] * 1e3
     if do_gather:
         # the rollout-end gather (RCCL all_gather_into_tensor, shard sizes from shard_bounds) of this
         # rollout's final observations [N, D] and every step's reward and done flags [K, N], right after the barrier
         # that closes the K timed steps, timed on every rank (max): `value` is the K steps (the bench contract),
         # `value_incl_gather` the rollout with its gather.  (Pipelined, opt-in: the previous rollout's observations
         # were gathered while these K steps ran, inside the timed region; the serial gather below then adds none.)
-        dst = dst if prev_obs is None else None
         tg_ms = 0.0
         if pending is None:
             torch.cuda.synchronize()
-            tg = time.perf_counter()
-            gathered = {"obs": gather_rollout(env.obs, n_total=world * N, dst=dst)}
-            if rec is not None:
-                gathered["reward"] = gather_rollout(rec["reward"], n_total=world * N, dim=1, dst=dst)
-                gathered["done"] = gather_rollout(rec["done"], n_total=world * N, dim=1, dst=dst)
+            tg = clock()
+            gathered = gather_all(env.obs)
             torch.cuda.synchronize()
-            tg_ms = max_over_ranks([time.perf_counter() - tg])[0] * 1e3
-        sent = {"obs": env.obs} if rec is None else {"obs": env.obs, "reward": rec["reward"], "done": rec["done"]}
+            tg_ms = pg.max_over_ranks([clock() - tg])[0] * 1e3
+            sent = {"obs": env.obs} if rec is None else {"obs": env.obs, "reward": rec["reward"], "done": rec["done"]}
+        else:
+            sent = {"obs": prev_obs}
+        # every rank's own results must be what landed in the gathered tensors (checksums of each rank's shard)
+        content = verify_gathered(sent, gathered, {"obs": 0, "reward": 1, "done": 1}, world * N, pg.host_group)
+        if not content["ok"]:
+            print(f"bench.py: gathered rollout does not match the ranks' own results: {content['mismatches']}",
+                  file=sys.stderr, flush=True)
+            sys.exit(3)
         gather_info = {"mode": args.gather, "to": ("rank 0 (dist.gather)" if dst == 0 else "every rank (all_gather)"),
                        "rows": world * N, "tensors": sorted(gathered),
                        "bytes_per_rank": int(sum(t.numel() * t.element_size() for t in sent.values())),
                        "gathered_bytes": int(world * sum(t.numel() * t.element_size() for t in sent.values())),
                        "ms": round(tg_ms, 4),
-                       **({"first_gather_ms": round(first_gather_ms, 3),
-                           "first_gather_note": ("the untimed gather before it: RCCL's communicator is created here"
-                                                 if backend == "nccl" else "the untimed gather before it")}
-                          if first_gather_ms is not None else {}),
                        "value_incl_gather": round(world * N * args.steps / (wall_max + tg_ms * 1e-3), 1),
+                       "content_check": content,
                        "note": "serial (default): this rollout's final observations [N, D] and its per-step reward "
                                "and done flags [K, N], gathered after the barrier closing the K timed steps, into "
                                "every rank (--gather-to root: to rank 0 only), ms = max over ranks; "
-                               "value_incl_gather = the K steps and this gather; pipelined (opt-in): the previous "
-                               "rollout's final observations gathered while these steps ran (inside the timed region)"}
+                               "value_incl_gather = the K steps and this gather; content_check: every rank's checksums "
+                               "of what it sent against its shard of the gathered tensors (a mismatch exits 3); "
+                               "pipelined (opt-in): the previous rollout's final observations gathered while these "
+                               "steps ran (inside the timed region)"}
 
-    comm_live_max = None
-    if in_world and backend == "nccl" and not comm_eager and graph is None:
-        # the same K steps again, now with RCCL's communicator up (the state has advanced; the work is the same):
-        # the rate of a later rollout of an actor that gathers every rollout
-        if not do_gather:   # (--no-gather: no collective has run yet; one small all-reduce creates the communicator)
-            dist.all_reduce(torch.zeros(1, device=dev))
-            torch.cuda.synchronize()
-        device_warm(stream, dev, warm_ms)
-        if args.warmup > 0:
-            env.run(acts_w, args.warmup, lanes=lanes)
+    # ---------------- sustained rate: the same prepared walker ranges, no extra device warm-up
+    sustained = None
+    B = bytes_per_walker_step(env.batch.host, bool(params.get("in3d")))
+    if graph is None and args.sustained_steps > 0:
+        S = args.sustained_steps
+        acts_s = acts[:S] if args.steps >= S else \
+            (torch.rand((S, N, A), generator=gen, device=dev) * 2 - 1).contiguous()
+        prep_s = env.prepare_run(acts_s, S, lanes=lanes)
         torch.cuda.synchronize()
-        if os.environ.get("WG_BENCH_BARRIER_BUSY", "1") != "0":
-            device_busy(stream, dev, 3)
-        barrier()
-        host_spin(float(os.environ.get("WG_BENCH_SPIN_US", "300")))
-        torch.cuda.synchronize()
-        tl = time.perf_counter()
-        prep()
-        torch.cuda.synchronize()
-        comm_live_max = max_over_ranks([time.perf_counter() - tl])[0]
+        runs = {}
+        t0s = open_region()
+        prep_s()
+        j1, _, _ = close_region(t0s)
+        reps = max(1, int(round(args.sustained_seconds / j1))) if args.sustained_seconds > 0 else 0
+        if in_world:
+            reps = int(pg.max_over_ranks([float(reps)])[0])
+        runs[f"k{S}"] = (S, j1)
+        if reps > 0:
+            t0s = open_region()
+            for _ in range(reps):
+                prep_s()
+            j2, _, _ = close_region(t0s)
+            runs["long"] = (S * reps, j2)
+        nf = None
+        if os.environ.get("WG_BENCH_CHECK_FINITE", "1") != "0":
+            # a blown-up walker would run the exact cold paths and time something else: every state must stay finite
+            nf = int((~torch.isfinite(env.batch.pos)).any().item() or (~torch.isfinite(env.batch.vel)).any().item())
+        head_v = world * N * args.steps / wall_max
+        sustained = {}
+        for key, (steps_, sec) in runs.items():
+            ms = sec * 1e3 / steps_
+            ach = B * N / (ms * 1e-3) / 1e9
+            sustained[key] = {"steps": steps_, "seconds": round(sec, 4), "ms_per_step": round(ms, 5),
+                              "value": round(world * N * steps_ / sec, 1), "achieved": round(ach, 1),
+                              "frac": round(ach / HBM_PEAK_GBS, 4)}
+        last = sustained["long" if "long" in sustained else f"k{S}"]
+        sustained["burst_over_sustained"] = round(head_v / last["value"], 4)
+        sustained["state_finite"] = None if nf is None else not bool(nf)
+        sustained["note"] = (f"after the K timed steps, in the same process: {S} steps (SURVEY §8(d)'s region) and then "
+                             f"the same {S}-step prepared run repeated back to back for ~{args.sustained_seconds:g} s "
+                             "('long'), with the headline's walker ranges and no extra device warm-up; job time as the "
+                             "headline (max over ranks of t1 - min of t0).  achieved / frac: N * B / ms_per_step (the "
+                             "two-range step) against 8 TB/s.  burst_over_sustained = value / long.value: the driver's "
+                             "K = 20 region runs at the GPU's burst clock, a long run at its sustained clock (DESIGN §6)."
+                             + (" Outputs overwritten each step (no per-step records)." if rec is not None else ""))
 
     if rank == 0:
         # single-launch control: one full-batch launch per step, HIP events on its stream — the per-dispatch
-        # duration a rocprofv3 kernel trace of `bench.py --lanes 1` reports (profiles/r02_*_kernel_stats*.csv)
+        # duration a rocprofv3 kernel trace of `bench.py --lanes 1` reports (profiles/*_kernel_groups.json)
         # (200 launches with their own distinct actions whatever K is: at a short K the first launches of a process
         # still see the clocks ramp, and the per-launch figure is the kernel's, not the bench's K)
         n1 = 200
@@ -579,6 +641,7 @@ def main():
         # at the end of every step, and every step returns obs/reward/done/info); the headline `value` instead
         # issues the K steps back to back (open loop: actions known up front, ranges drift out of phase)
         closed_ms = None
+        open_ms = None
         if not args.no_control:
             n_cl = n1
             for s_ in range(5):
@@ -590,6 +653,17 @@ def main():
             e1.record(stream)
             torch.cuda.synchronize()
             closed_ms = e0.elapsed_time(e1) / n_cl
+            # the open loop over the same 200-step region the closed loops below are timed on (VERDICT r5 item 1:
+            # like with like), the headline's walker ranges and prepared call
+            prep_c = env.prepare_run(acts_c, n1, lanes=lanes)
+            prep_c()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            prep_c()
+            e1.record(stream)
+            torch.cuda.synchronize()
+            open_ms = e0.elapsed_time(e1) / n1
         # closed loop with a policy (every action a function of the current observation): a row-wise policy, tanh of
         # each walker's observed muscle lengths, driven (a) by step() in a loop — one barrier per step — and (b) by
         # policy_loop, the walker ranges pipelined (each range acts on its own rows and steps on its own stream);
@@ -652,17 +726,21 @@ def main():
                                     "policy_loop splits the ranges where their walkers are caller-contiguous (a range "
                                     "elsewhere gathers its rows and scatters its actions)"),
                          "steps": n1,
+                         "open_loop_ms_per_step": round(open_ms, 5),
                          "step_loop_ms_per_step": round(step_pol_ms, 5),
                          "policy_loop_ms_per_step": round(ranges_ms, 5),
                          "policy_loop_graph_ms_per_step": round(ranges_graph_ms, 5),
                          "policy_loop_null_policy_ms_per_step": round(null_ms, 5),
+                         "policy_loop_over_open_loop": round(ranges_ms / open_ms, 4),
                          "lanes": lanes,
-                         "note": "step_loop: BatchedPhysicsEnv.step(policy(obs)) per env step (a full barrier per step: each "
+                         "note": "every figure over the same 200-step region (HIP events): open_loop: the prepared run "
+                                 "of the headline's walker ranges with the actions known up front; step_loop: "
+                                 "BatchedPhysicsEnv.step(policy(obs)) per env step (a full barrier per step: each "
                                  "launch drains alone); policy_loop: the walker ranges pipelined, each range's policy "
                                  "and step on its own stream (bit-identical trajectories, tests/test_gpu_policy_loop.py); "
                                  "graph: the same loop captured as one HIP graph per walker range, each replayed on its "
-                                 "own stream (HIP events around the replay); null_policy: policy_loop with a policy that "
-                                 "launches nothing (the loop's own cost against the open loop)"}
+                                 "own stream; null_policy: policy_loop with a policy that launches nothing (the loop's "
+                                 "own cost against the open loop)"}
         resident_ms = None
         if args.resident:
             env.run(acts_c, n1, lanes=1, resident=True)
@@ -673,7 +751,6 @@ def main():
             torch.cuda.synchronize()
             resident_ms = e0.elapsed_time(e1) / args.steps
         D = env.obs_dim
-        B = bytes_per_walker_step(env.batch.host, bool(params.get("in3d")))
         M, K = env.batch.M, env.batch.K
         uniform = not env.batch.ragged
         if uniform:
@@ -695,18 +772,20 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(wall_max * 1e3 / args.steps, 5),
-            "timing": {"clock": "wall, t0 after barrier + synchronize, t1 after each rank's synchronize; max over ranks",
+            "timing": {"clock": ("host CLOCK_MONOTONIC, one clock for the node's ranks: t0 after the opening barrier + "
+                                 "synchronize, t1 after each rank's synchronize; job time = max(t1) - min(t0) over "
+                                 "ranks (start skew included)" if in_world else
+                                 "host CLOCK_MONOTONIC: t0 after synchronize, t1 after synchronize"),
+                       "ms_per_step_slowest_rank": round(slowest_rank * 1e3 / args.steps, 5),
                        "ms_per_step_incl_closing_barrier": round(wall_bar_max * 1e3 / args.steps, 5),
                        "device_warm_ms": round(warm_s * 1e3, 2),
                        "kernel_ms_per_step_events": round(step_ms, 5),
-                       **({"comm": "RCCL's communicator created by the first gather, after the timed steps; barriers "
-                                   "and the max over ranks on a gloo group",
-                           "comm_live_ms_per_step": round(comm_live_max * 1e3 / args.steps, 5),
-                           "comm_live_value": round(world * N * args.steps / comm_live_max, 1),
-                           "comm_live_note": "the same K steps timed again after the gather, communicator up, same "
-                                             "warm-up (DESIGN §8)"} if comm_live_max is not None else
-                          {"comm": ("RCCL's communicator created before the timed steps" if backend == "nccl" else
-                                    f"{backend} process group (rehearsal, no RCCL)")} if in_world else {})},
+                       "region": "burst: a K-step region after a 100 ms device warm-up runs at the GPU's burst clock; "
+                                 "`sustained` times 1,000 steps and a ~2 s run of the same walker ranges beside it",
+                       **({"comm": "RCCL's communicator up before the timed steps (created and checked by a one-element "
+                                   "all_reduce, then one untimed gather of the rollout's tensors); barriers and the "
+                                   "clock exchange on a gloo group"} if in_world and backend == "nccl" else
+                          {"comm": f"{backend} process group (rehearsal, no RCCL)"} if in_world else {})},
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -718,9 +797,10 @@ def main():
                                    f"({lanes} range{'s' if lanes > 1 else ''} on {lanes} stream{'s' if lanes > 1 else ''})"
                                    + (", replayed as one HIP graph" if graph is not None else ""),
                        "walkers_per_gpu": N, "total_walkers": world * N, "M": M, "K": K, "A": env.batch.A,
-                       "obs_dim": D, "parallelism": f"dp{world}", "rollout_gather": (args.gather if gathered is not None else False),
+                       "obs_dim": D, "parallelism": f"dp{world}",
+                       "rollout_gather": (args.gather if gathered is not None else False),
                        "dist_backend": (dist.get_backend() if in_world else None),
-                       **({"dist_init": "before the env" if dist_first else "after the env's streams and warm-up"}
+                       **({"dist_init": "before the env" if dist_first else "after the env's streams and first step"}
                           if in_world else {}),
                        "lanes": lanes, "launch": geo, "ragged_kind": env.batch.ragged_kind,
                        **({"chain_points": args.chain_points, "pair_mode": params["pair_mode"]}
@@ -738,36 +818,31 @@ def main():
                                   "no single-launch timing); B = SURVEY §8(d) algorithmic bytes averaged over the "
                                   "walkers")},
         }
+        if comm is not None:
+            line["comm"] = comm
+        if sustained is not None:
+            line["sustained"] = sustained
         if lanes > 1 or graph is not None:
             a2 = B * N / (step_ms * 1e-3) / 1e9
             line["roofline"]["concurrent"] = {
                 "lanes": lanes, "kernel_ms_per_step_events": round(step_ms, 5), "achieved": round(a2, 1),
                 "frac": round(a2 / HBM_PEAK_GBS, 4),
                 "note": f"{lanes} walker ranges on {lanes} streams overlap one range's launch tail with the other's "
-                        "next step: HIP events around the K timed steps"}
-            win = load_window(args.workload, N, lanes) if graph is None else None
-            if win:
-                a3 = B * N / (win["us_per_step"] * 1e-6) / 1e9
-                line["roofline"]["concurrent"]["rocprof"] = {
-                    "us_per_step": win["us_per_step"], "achieved": round(a3, 1), "frac": round(a3 / HBM_PEAK_GBS, 4),
-                    "share_two_or_more_running": win.get("share_two_or_more_running"), "queues": win.get("queues"),
-                    "source": win["file"],
-                    "note": "the same timed region in a rocprofv3 --kernel-trace of this bench (an earlier run, "
-                            "committed): span of its launches by their own timestamps / K (scripts/trace_kernels.py "
-                            "--window)"}
+                        "next step: HIP events around the K timed steps (burst region; `sustained` has the long-run "
+                        "fraction)"}
         if graph is not None:
             line["graph"] = {"replay_ms_per_step": round(step_ms, 5), "direct_ms_per_step": round(direct_ms, 5),
                              "launch_overhead_share": round(max(0.0, 1 - step_ms / direct_ms), 4)}
         if closed_ms is not None:
             line["closed_loop"] = {
                 "ms_per_step": round(closed_ms, 5), "env_steps_per_s": round(N * 1e3 / closed_ms, 1),
+                "open_loop_ms_per_step": round(open_ms, 5),
                 "lanes": env._step_lanes(),
                 "note": "BatchedPhysicsEnv.step() once per env step (HIP events on the calling stream over 200 "
                         "steps; one walker range, step()'s default): each step returns obs / reward / done / info "
-                        "— what a PhysicsEnv.step caller gets; `value` is the open-loop rate (K steps issued back "
-                        "to back on the ranges of run())"}
+                        "— what a PhysicsEnv.step caller gets; open_loop: the headline's prepared walker ranges over "
+                        "the same 200 steps"}
         if policy_cl is not None:
-            policy_cl["open_loop_ms_per_step"] = round(step_ms, 5)
             line["closed_loop_policy"] = policy_cl
         if resident_ms is not None:
             line["resident_rollout"] = {

@@ -86,6 +86,15 @@ def test_errors_without_gpu(lib):
     with pytest.raises(ValueError):
         _lib.check(-1, "probe")
     assert lib.wg_reset_noise(None, None, None) == _lib.WG_EINVAL
+    # SURVEY §8(b)'s declared signatures (ABI 13): the same checks, and ragged batches refused (no plan argument)
+    assert lib.wg_step_simple(None, None, C.byref(p), 1, None) == _lib.WG_EINVAL
+    assert b"null batch" in lib.wg_last_error()
+    assert lib.wg_observe_simple(C.byref(_lib.WgBatch(N=4, M=8, K=4, A=0)), None, None, None, None, None, None,
+                                 None) == _lib.WG_EINVAL
+    rb = _lib.WgBatch(N=4, M=8, K=4, A=0, ragged=2)
+    assert lib.wg_step_simple(C.byref(rb), None, C.byref(p), 1, None) == _lib.WG_EINVAL
+    assert b"uniform batches only" in lib.wg_last_error()
+    assert lib.wg_observe_simple(C.byref(rb), C.byref(p), None, None, None, None, None, None) == _lib.WG_EINVAL
     # pair passes need the engine.py spring (spring_mode 0): refused before any launch
     b = _lib.WgBatch(N=4, M=8, K=4, A=0, ragged=1)
     for f in ("pos", "vel", "acc", "mass", "edges", "inc", "inc_off", "muscle_x", "steps", "mass_off", "edge_off",

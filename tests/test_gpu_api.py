@@ -128,3 +128,44 @@ def test_step_ranges_validates_every_range_before_launching():
     torch.cuda.synchronize()
     assert rc == _lib.WG_EINVAL
     assert torch.equal(env.pos, before) and torch.equal(env.steps, steps0)
+
+
+@pytest.mark.parametrize("workload", ["canonical", "balance2d"])
+def test_survey_signature_entry_points_bit_exact(workload):
+    """SURVEY §8(b)'s declared signatures (ABI 13): wg_step_simple(batch, action, params, n_steps, stream) for T steps
+    with [T, N, A] actions in one call, then wg_observe_simple(batch, cfg, obs, reward, done, centroid, energy, stream),
+    bit-identical to the same walkers stepped by BatchedPhysicsEnv.run (wg_run_ranges) — state, step counters and
+    every output; a ragged batch is refused."""
+    import ctypes as C
+    import torch
+    from walker_gym_amd import _lib
+    from walker_gym_amd.batched_env import BatchedPhysicsEnv
+    from walker_gym_amd.synthetic import canonical_walkers, ragged_walkers
+    from walker_gym_amd.walker import balance_spec
+    spec, kw = (canonical_walkers(640, seed=11), dict(in3d=1)) if workload == "canonical" else (balance_spec(640), dict(in3d=0))
+    a_env = BatchedPhysicsEnv(spec, device="cuda:0", **kw)
+    b_env = BatchedPhysicsEnv(spec, device="cuda:0", **kw)
+    T, N, A = 25, a_env.N, a_env.batch.A
+    g = torch.Generator(device="cuda:0").manual_seed(5)
+    acts = (torch.rand((T, N, A), generator=g, device="cuda:0") * 2 - 1).contiguous()
+    a_env.run(acts, T)
+    L = _lib.load()
+    st = torch.cuda.current_stream().cuda_stream
+    assert L.wg_step_simple(C.byref(b_env.batch.struct), acts.data_ptr(), C.byref(b_env._pstruct), T, st) == 0
+    obs = torch.full((N, a_env.obs_dim), -7.0, device="cuda:0")
+    rew = torch.empty(N, device="cuda:0")
+    done = torch.empty(N, dtype=torch.uint8, device="cuda:0")
+    cen = torch.empty((N, 3), device="cuda:0")
+    en = torch.empty(N, device="cuda:0")
+    assert L.wg_observe_simple(C.byref(b_env.batch.struct), C.byref(b_env._pstruct), obs.data_ptr(), rew.data_ptr(),
+                               done.data_ptr(), cen.data_ptr(), en.data_ptr(), st) == 0
+    torch.cuda.synchronize()
+    for name in ("pos", "vel", "acc", "muscle_x", "steps"):
+        assert torch.equal(getattr(a_env, name), getattr(b_env, name)), name
+    bits = lambda t: t.contiguous().view(torch.int32)
+    assert torch.equal(bits(obs), bits(a_env.obs))
+    assert torch.equal(bits(rew), bits(a_env.reward)) and torch.equal(done.bool(), a_env.done)
+    assert torch.equal(bits(cen), bits(a_env.centroid)) and torch.equal(bits(en), bits(a_env.energy))
+    r_env = BatchedPhysicsEnv(ragged_walkers(64, seed=2, mmin=4, mmax=12), device="cuda:0", in3d=1)
+    assert L.wg_step_simple(C.byref(r_env.batch.struct), None, C.byref(r_env._pstruct), 1, st) == _lib.WG_EINVAL
+    assert b"uniform batches only" in L.wg_last_error()

@@ -231,3 +231,16 @@ def test_bounce_set_packing():
     lay = pack(dict(rg, bounce_set=bsr))
     assert np.array_equal(lay.bounce_set[lay.mass_perm], bsr) if lay.mass_perm is not None else \
         np.array_equal(lay.bounce_set, bsr)
+
+
+def test_bounce_set_from_lists():
+    """The converter from the reference's calls (`for p in callers: p.bounce(k, other=L)`) to bounce_set bytes: callers
+    and one shared list, both in registry order; lists the two bits cannot express (another order, repeats, bad
+    indices) are refused rather than silently reordered."""
+    from walker_gym_amd.layout import bounce_set_from_lists
+    assert bounce_set_from_lists(5, [0, 2, 4]).tolist() == [3, 2, 3, 2, 3]
+    assert bounce_set_from_lists(5, [1, 3], [0, 1, 4]).tolist() == [2, 3, 0, 1, 2]
+    assert bounce_set_from_lists(4, [], []).tolist() == [0, 0, 0, 0]
+    for callers, other in (([2, 1], "*"), ([0], [3, 1]), ([0], [1, 1]), ([0, 0], "*"), ([5], "*"), ([0], "all")):
+        with pytest.raises(ValueError):
+            bounce_set_from_lists(5, callers, other)

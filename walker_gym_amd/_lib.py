@@ -13,7 +13,7 @@ import threading
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libwalker_hip.so"
 LIB_PATH = os.path.join(HERE, LIB_NAME)
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 WG_EINVAL, WG_ERANGE, WG_EHIP = -1, -2, -3
 
@@ -59,8 +59,9 @@ class WgLaunchInfo(C.Structure):
                 ("lds_bytes", C.c_int32)]
 
 
-EXPORTS = ("wg_abi_version", "wg_last_error", "wg_step", "wg_step_ranges", "wg_run_ranges", "wg_rollout", "wg_observe", "wg_reset", "wg_reset_noise",
-           "wg_plan_ragged", "wg_plan_waves", "wg_wave_edge_passes", "wg_plan_errors", "wg_launch_geometry", "wg_launch_floor")
+EXPORTS = ("wg_abi_version", "wg_last_error", "wg_step", "wg_step_ranges", "wg_run_ranges", "wg_rollout", "wg_observe",
+           "wg_step_simple", "wg_observe_simple", "wg_reset", "wg_reset_noise", "wg_plan_ragged", "wg_plan_waves",
+           "wg_wave_edge_passes", "wg_plan_errors", "wg_launch_geometry", "wg_launch_floor")
 
 _lib = None
 _lock = threading.Lock()
@@ -92,6 +93,9 @@ def load(path: str | None = None):
         L.wg_run_ranges.argtypes = [C.POINTER(WgRange), C.c_int32, C.POINTER(WgParams), _vp, C.c_int32, C.c_int32,
                                     C.c_int64, C.c_int32, C.POINTER(_vp)]
         L.wg_observe.argtypes = [C.POINTER(WgBatch), C.POINTER(WgParams), C.POINTER(WgOutputs), _vp, C.c_int32, _vp]
+        # SURVEY §8(b)'s declared signatures (ABI 13)
+        L.wg_step_simple.argtypes = [C.POINTER(WgBatch), _vp, C.POINTER(WgParams), C.c_int32, _vp]
+        L.wg_observe_simple.argtypes = [C.POINTER(WgBatch), C.POINTER(WgParams), _vp, _vp, _vp, _vp, _vp, _vp]
         L.wg_reset.argtypes = [C.POINTER(WgBatch), C.POINTER(WgParams), _vp, _vp, _vp]
         L.wg_reset_noise.argtypes = [C.POINTER(WgBatch), _vp, _vp]
         L.wg_plan_ragged.argtypes = [_vp, _vp, _vp, C.c_int32, _vp, C.c_int32]
@@ -100,8 +104,7 @@ def load(path: str | None = None):
         L.wg_plan_errors.argtypes = [C.c_int32]
         L.wg_launch_geometry.argtypes = [C.POINTER(WgBatch), C.POINTER(WgLaunchInfo)]
         L.wg_launch_floor.argtypes = [C.c_int32, C.c_int32, C.c_int32, _vp, _vp, C.c_int32, _vp]
-        for f in ("wg_step", "wg_step_ranges", "wg_run_ranges", "wg_rollout", "wg_observe", "wg_reset", "wg_reset_noise", "wg_plan_ragged", "wg_plan_waves",
-                  "wg_wave_edge_passes", "wg_plan_errors", "wg_launch_geometry", "wg_launch_floor"):
+        for f in EXPORTS[2:]:
             getattr(L, f).restype = C.c_int
         v = L.wg_abi_version()
         if v != ABI_VERSION:

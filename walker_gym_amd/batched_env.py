@@ -506,6 +506,9 @@ class BatchedPhysicsEnv:
         # the opt-in info extras follow the last step only when the outputs are overwritten each step (no record)
         o = self._outputs(self.obs, rew, done, cen, en, pad_clean=True, steps=so, out_step=out_step,
                           **(self._extra_out() if (info and record is None) else {}))
+        # every tensor whose raw pointer sits in `o`, held by the PreparedRun (a caller that drops its record
+        # buffers and calls the PreparedRun again must not have the kernel write into freed memory)
+        pins = [self.obs, so, actions, *(() if record is None else record.values()), *self._extra_out().values()]
         steps_valid = so is not None
         n_steps = int(n_steps)
         if lanes > 1:
@@ -516,17 +519,17 @@ class BatchedPhysicsEnv:
                 if n_steps > 0:
                     for st in self._side[:lanes - 1]:
                         actions.record_stream(st)   # the allocator must not recycle it before the side streams are done
-                return PreparedRun(self, "wg_run_ranges", fn, args, keep, steps_valid, stale)
+                return PreparedRun(self, "wg_run_ranges", fn, args, keep + pins, steps_valid, stale)
             # (range-by-range issue, a resident rollout over several ranges, or a graph capture: one C call per range)
-            return PreparedRun(self, entry, None, (actions, n_steps, o, lanes, entry, _only), [o], steps_valid, stale,
-                               thunk=self._run_lanes)
+            return PreparedRun(self, entry, None, (actions, n_steps, o, lanes, entry, _only), [o] + pins, steps_valid,
+                               stale, thunk=self._run_lanes)
         # (a resident launch writes the steps output only where the resident kernel runs: uniform batches, which
         # have no steps_out)
         args = (C.byref(self.batch.struct), C.byref(self._pstruct), actions.data_ptr(), cols, cols,
                 0 if T == 1 else self.N * cols, C.byref(o), n_steps,
                 None if self.batch.plan is None else self.batch.plan.data_ptr(), self.batch.plan_blocks,
                 torch.cuda.current_stream(self.device).cuda_stream)
-        return PreparedRun(self, entry, getattr(_lib.load(), entry), args, [o, actions], steps_valid, stale)
+        return PreparedRun(self, entry, getattr(_lib.load(), entry), args, [o] + pins, steps_valid, stale)
 
     def _lanes(self, lanes: Optional[int]) -> int:
         """Walker ranges run() steps on separate streams (ragged batches: ranges of plan blocks).  Default 2 for
@@ -740,8 +743,13 @@ class BatchedPhysicsEnv:
             rng = list(enumerate(args)) if only is None else [(only, args[only])]
             shapes = [None] * lanes
             dix = dev.index
-            abuf = None   # scattered ragged ranges: the [N, A] action buffer they scatter into (allocated at the first
-            #               step, on the calling stream, which every range's stream joins at the end)
+            # scattered ragged ranges: the [N, A] action buffer they scatter into.  Its columns are known only from the
+            # first policy call, so it is allocated then, on `cur` (uninitialised: every range writes its own rows
+            # before its step reads them), and an event recorded on `cur` right after the allocation orders every
+            # stream that touches it after whatever `cur` ran in that memory before (the caching allocator reuses a
+            # block freed on `cur` without waiting for other streams); the ranges' streams join `cur` at the end, so
+            # its release on `cur` is ordered after their last reads
+            abuf, abuf_ev, abuf_ok = None, None, set()
             try:
                 for t in range(int(n_steps)):
                     for (r, (obs_r, idx, n_r, b_ref, o_ref, plan, nblk)), (st, st_ptr) in zip(rng, sts):
@@ -762,7 +770,15 @@ class BatchedPhysicsEnv:
                         cols = a.shape[1]
                         if idx is not None:   # a scattered ragged range: its caller rows of the action buffer
                             if abuf is None:
-                                abuf = torch.zeros((self.N, cols), dtype=f32, device=dev)
+                                with torch.cuda.stream(cur):
+                                    abuf = torch.empty((self.N, cols), dtype=f32, device=dev)
+                                abuf_ok.add(cur.cuda_stream)
+                                if multi:   # (one stream, e.g. a captured range: nothing to order)
+                                    abuf_ev = torch.cuda.Event()
+                                    abuf_ev.record(cur)
+                            if abuf_ev is not None and st_ptr not in abuf_ok:
+                                st.wait_event(abuf_ev)
+                                abuf_ok.add(st_ptr)
                             abuf.index_copy_(0, idx, a)
                             a_ptr = abuf.data_ptr()
                         else:                 # (rows aoff[r] .. of the caller's order: the pointer moved back)

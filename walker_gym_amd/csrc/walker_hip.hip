@@ -1782,6 +1782,8 @@ struct LeanGeo {
     int off_df, off_inc, off_x;               // byte offsets in the slice (spring terms at 0)
     int pl;                                   // spring-term slots of a wave tile (>= wpw * K, multiple of 4)
     float invK, invA, invM;                   // invM = 1/M, exact (M | 64 is a power of two)
+    int nblk;                                 // the launch's workgroup count (xcd_block), an explicit argument: read
+                                              // from the dispatch packet it costs a dependent scalar round
 };
 
 // LDS hand-off between lanes of ONE wave: a wave's LDS operations execute in order, so a compiler
@@ -2434,7 +2436,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lean_waves(
     // the wave index as a wave-uniform (scalar) value: the tile's walker range and element bases are then SALU
     // products, not per-lane v_mul_lo_u32
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#ifdef WG_AB_GRIDDIM   // TEMPORARY A/B (round 6): HEAD's prologue
     const int blk = (kp.xcd & 2) ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+#else
+    // NE = 1 (the latency-bound small batches): every kernel argument the tile's loads need, in SGPRs before anything
+    // else.  Left to the compiler they come in three dependent scalar rounds (the XCD-order arguments, then the batch
+    // shape after that arithmetic, then the array bases after the early exit) before the first vector load.  (Not at
+    // NE >= 2: the pinned bases cost those instances 11 VGPRs, 67 -> 78 at NE = 3.)
+#ifndef WG_AB_NOASM   // TEMPORARY A/B (round 6)
+    if (NE == 1)
+        asm volatile("" ::"s"(b.N), "s"(b.M), "s"(b.K), "s"(b.A), "s"(b.pos), "s"(b.vel), "s"(b.edges), "s"(b.inc),
+                     "s"(b.inc_off), "s"(b.mass), "s"(b.steps), "s"(b.muscle_x), "s"(b.muscle_bounds), "s"(action),
+                     "s"(action_stride), "s"(action_cols), "s"(kp.prio), "s"(kp.xcd), "s"(lg.nblk), "s"(lg.wpb),
+                     "s"(lg.wpw));
+#endif
+    const int bid = blockIdx.x, xb = xcd_block(bid, lg.nblk);
+    const int blk = (kp.xcd & 2) ? xb : bid;
+#endif
     const int tile = blk * lg.wpb + wv;
     if (tile * lg.wpw >= b.N) return;
 #ifdef WG_STAMPS
@@ -3090,6 +3108,7 @@ bool lean_geo(const wg_batch *b, int obs_stride, LeanGeo *out, int spring_mode =
     g.invK = 1.f / (float)b->K;
     g.invA = 1.f / (float)std::max(1, b->A);
     g.invM = 1.f / (float)M;
+    g.nblk = (b->N + g.wpb * g.wpw - 1) / (g.wpb * g.wpw);   // = lean_blocks
     *out = g;
     return true;
 }
@@ -3368,6 +3387,28 @@ int wg_observe(const wg_batch *b, const wg_params *p, const wg_outputs *o, const
                int32_t plan_blocks, hipStream_t stream) {
     if (!o) return fail(WG_EINVAL, "null outputs");
     return run(b, p, nullptr, 0, 0, 0, o, 1, plan, plan_blocks, stream, false);
+}
+
+// SURVEY §8(b)'s declared signatures (ABI 13): uniform batches only (a ragged batch needs a plan)
+int wg_step_simple(const wg_batch *b, const float *action, const wg_params *p, int32_t n_steps, hipStream_t stream) {
+    if (b && b->ragged) return fail(WG_EINVAL, "wg_step_simple: uniform batches only (ragged: wg_step with a plan)");
+    const int32_t A = b ? b->A : 0;
+    const int64_t step = b ? (int64_t)b->N * A : 0;
+    return run(b, p, A > 0 ? action : nullptr, A, A, step, nullptr, n_steps, nullptr, 0, stream, true);
+}
+
+int wg_observe_simple(const wg_batch *b, const wg_obs_cfg *cfg, float *obs, float *reward, uint8_t *done,
+                      float *centroid, float *energy, hipStream_t stream) {
+    if (b && b->ragged) return fail(WG_EINVAL, "wg_observe_simple: uniform batches only (ragged: wg_observe with a plan)");
+    if (!b || !cfg) return fail(WG_EINVAL, "null batch / cfg");
+    wg_outputs o{};
+    o.obs = obs;
+    o.obs_stride = 3 * (cfg->in3d ? 3 : 2) * b->M + (cfg->conmid ? 3 : 0) + b->A;
+    o.reward = reward;
+    o.done = done;
+    o.centroid = centroid;
+    o.energy = energy;
+    return run(b, cfg, nullptr, 0, 0, 0, &o, 1, nullptr, 0, stream, false);
 }
 
 int wg_reset(const wg_batch *b, const wg_params *p, const float *noise, const uint8_t *mask, hipStream_t stream) {

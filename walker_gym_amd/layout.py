@@ -226,10 +226,37 @@ def default_radius(mass: np.ndarray) -> np.ndarray:
     return np.asarray(mass, np.float32).astype(np.float64) ** 0.3
 
 
+def bounce_set_from_lists(n_points: int, callers, other="*") -> np.ndarray:
+    """One walker's `bounce_set` bytes from the reference's calls `for p in callers: p.bounce(k, other=other)`
+    (gym/engine.py:114-126), as point indices of the walker.  The two-bit encoding holds exactly this: the callers in
+    registry order (ascending, each once) and ONE `other` list shared by every caller, in registry order (ascending,
+    each once; "*" = every point).  The reference iterates `other` in the order given and float32 accumulation
+    follows that order, so a list in any other order, with a repeated point, or different per caller changes the
+    reference's bits and is not expressible: it raises ValueError instead of silently reordering."""
+    def idx(lst, what):
+        a = np.asarray(list(lst), np.int64).reshape(-1)
+        if a.size and (a.min() < 0 or a.max() >= n_points):
+            raise ValueError(f"bounce {what}: point index out of range [0, {n_points})")
+        if a.size > 1 and not bool(np.all(np.diff(a) > 0)):
+            raise ValueError(f"bounce {what} must be in registry order (ascending point indices, no repeats): the "
+                             "reference iterates the list as given, which bounce_set cannot express otherwise")
+        return a
+    bs = np.zeros(n_points, np.uint8)
+    bs[idx(callers, "callers")] |= 1
+    if isinstance(other, str):
+        if other != "*":
+            raise ValueError('bounce other must be "*" or a list of point indices')
+        bs |= 2
+    else:
+        bs[idx(other, "other")] |= 2
+    return bs
+
+
 def _bounce_set(spec, P: int):
     """Per point, which side of Point.bounce(k, other=<list>) it is on: bit 0 the point calls bounce (callers in
     registry order), bit 1 it is in `other` (the list in registry order); other bits must be 0.  All 3 is the
-    reference's default other="*" and is stored as None."""
+    reference's default other="*" and is stored as None.  Restriction: one shared `other` list per walker, iterated in
+    registry order (bounce_set_from_lists builds the bytes and rejects what they cannot express)."""
     bs = spec.get("bounce_set")
     if bs is None:
         return None

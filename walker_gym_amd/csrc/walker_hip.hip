@@ -55,6 +55,12 @@ constexpr int MAXT = 512;               // __launch_bounds__: workgroups are 64.
 #ifndef WG_ABLATE
 #define WG_ABLATE 0
 #endif
+#ifndef WG_AB_NODEAD   // TEMPORARY A/B (round 6): 1 = no diverged-walker stand-in path
+#define WG_AB_NODEAD 0
+#endif
+#ifndef WG_AB_PRELOAD  // TEMPORARY A/B (round 6): 1 = NE = 1 with preloaded leading kernel arguments
+#define WG_AB_PRELOAD 0
+#endif
 
 // Float32 constants derived from wg_params exactly where numpy rounds the Python scalars.
 struct KParams {
@@ -2232,6 +2238,28 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
     wave_sync();
     STAMP(2);
 
+    // ================= diverged walkers (round 6): every mass of the walker has a NaN position component, is not pinned
+    // and has a spring.  Then every spring term of the walker is NaN (norm, dx, f and the direction all are: Python's
+    // max(NaN, r) keeps NaN, gym/engine.py:73-75), so each mass's a, and after run1 its v and pos, are NaN in all three
+    // components; its contact test (pos_y - ground < 0) is false; the muscle lengths still follow the actions.  The
+    // walker's lanes step benign finite stand-ins (mass q at (q, 0, 0), at rest) so that no exact cold path runs for it,
+    // and its state, outputs and sums are then set to what the reference computes: NaN (NaN payloads aside).  A
+    // walker only partly NaN, or with an inf, steps exactly as before.  Pair passes keep the plain path.
+    bool dead = false;
+    if (!RES && kp.pair_mode == 0 && !WG_AB_NODEAD) {
+        const bool dm = is_mass && !pin && L.io1 > L.io0 &&
+                        (__builtin_isnan(L.p3[0]) || __builtin_isnan(L.p3[1]) || __builtin_isnan(L.p3[2]));
+        const unsigned long long db = __ballot(dm);
+        if (__builtin_expect(db != 0ull, 0)) {   // wave-uniform, rare
+            const unsigned long long gm = (M == 64) ? ~0ull : (((1ull << M) - 1ull) << (lane & ~(M - 1)));
+            dead = is_mass && (db & gm) == gm;
+            if (dead) {
+                L.p3[0] = (float)q; L.p3[1] = 0.f; L.p3[2] = 0.f;
+                L.v3[0] = 0.f; L.v3[1] = 0.f; L.v3[2] = 0.f;
+            }
+        }
+    }
+
     // ================= springs: gym/engine.py:78-102 + gym/optimized_walker.py:92-106 =================
     bool gtiny = false;   // a damping force of this lane's springs outside the mass loop's exact quotient range
     const bool pos_ok = __all(fexp3(L.p3[0], L.p3[1], L.p3[2]) >= -55);   // (spring_terms)
@@ -2319,14 +2347,18 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
     if (is_mass) {
         mass_tail(kp, mf, (float)ym, L.p3, L.v3, px, py, pz, vx, vy, vz, ax, ay, az, hit, pin,
                   !RES ? &et : nullptr);
+        if (dead) {   // (a diverged walker, above: what the reference computes)
+            px = __builtin_nanf(""); py = px; pz = px; vx = px; vy = px; vz = px; ax = px; ay = px; az = px;
+            hit = false;
+        }
         if (b.radius && store) b.radius[pl] = hit ? 3.0 : 1.0;   // p.r = 3 / p.r = 1 (gym/optimized_env.py:156,175)
         nv = np_norm3(vx, vy, vz);
-        if (!(NE == 1 && !RES)) ke = mf * np_sq<NE == 1>(nv);   // p.m * norm(p.v) ** 2 (gym/optimized_env.py:242)
+        if (!(NE == 1 && !RES)) ke = dead ? nv : mf * np_sq<NE == 1>(nv);   // p.m * norm(p.v) ** 2 (optimized_env.py:242)
         pe = (float)((double)mf * kp.g) * (py - kp.ground);
     }
     if (NE == 1 && !RES) {   // every lane (table gathers); lanes past the masses square 0
-        const float sq = np_sq_wave(nv, sq_tl, sq_te);
-        if (is_mass) ke = mf * sq;
+        const float sq = np_sq_wave(dead ? 0.f : nv, sq_tl, sq_te);
+        if (is_mass) ke = dead ? nv : mf * sq;
     }
     STAMP(4);
 
@@ -2436,23 +2468,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lean_waves(
     // the wave index as a wave-uniform (scalar) value: the tile's walker range and element bases are then SALU
     // products, not per-lane v_mul_lo_u32
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#ifdef WG_AB_GRIDDIM   // TEMPORARY A/B (round 6): HEAD's prologue
-    const int blk = (kp.xcd & 2) ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
-#else
     // NE = 1 (the latency-bound small batches): every kernel argument the tile's loads need, in SGPRs before anything
     // else.  Left to the compiler they come in three dependent scalar rounds (the XCD-order arguments, then the batch
-    // shape after that arithmetic, then the array bases after the early exit) before the first vector load.  (Not at
-    // NE >= 2: the pinned bases cost those instances 11 VGPRs, 67 -> 78 at NE = 3.)
-#ifndef WG_AB_NOASM   // TEMPORARY A/B (round 6)
-    if (NE == 1)
+    // shape after that arithmetic, then the array bases after the early exit) before the first vector load.
+    // Balance-4096, one launch per step, same box, 7 interleaved rounds (profiles/r06b_ab_balance4096_prologue.json):
+    // 5.01 us against 5.33 with round 5's prologue and 5.52 with the explicit workgroup count alone.  NE >= 2 keeps
+    // round 5's prologue instruction for instruction (the pinned bases would cost those instances 11 VGPRs, 67 -> 78
+    // at NE = 3).
+    int blk;
+    if (NE == 1) {
         asm volatile("" ::"s"(b.N), "s"(b.M), "s"(b.K), "s"(b.A), "s"(b.pos), "s"(b.vel), "s"(b.edges), "s"(b.inc),
                      "s"(b.inc_off), "s"(b.mass), "s"(b.steps), "s"(b.muscle_x), "s"(b.muscle_bounds), "s"(action),
                      "s"(action_stride), "s"(action_cols), "s"(kp.prio), "s"(kp.xcd), "s"(lg.nblk), "s"(lg.wpb),
                      "s"(lg.wpw));
-#endif
-    const int bid = blockIdx.x, xb = xcd_block(bid, lg.nblk);
-    const int blk = (kp.xcd & 2) ? xb : bid;
-#endif
+        const int bid = blockIdx.x, xb = xcd_block(bid, lg.nblk);   // (the workgroup count as an explicit argument)
+        blk = (kp.xcd & 2) ? xb : bid;
+    } else {
+        blk = (kp.xcd & 2) ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    }
     const int tile = blk * lg.wpb + wv;
     if (tile * lg.wpw >= b.N) return;
 #ifdef WG_STAMPS
@@ -2468,6 +2501,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lean_waves(
     STAMP(1);
     lean_compute<IN3D, NE>(b, kp, o, lg, smem + wv * lg.slice, t, lane, L);
 }
+
+#if WG_AB_PRELOAD   // TEMPORARY A/B (round 6): NE = 1 with its leading arguments preloaded into SGPRs by the dispatch
+// (-mllvm -amdgpu-kernarg-preload-count=10 preloads leading pointer / scalar arguments only, <= 14 SGPRs: these ten,
+// everything the tile index and the first vector loads need; nblkx = the workgroup count | the XCD-order flag << 30 |
+// the load-phase priority flag << 31)
+template <bool IN3D>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lean_waves(1)))) void walker_step_lean_pre(
+    float *pos, float *vel, const wg_edge *edges, const uint16_t *inc, int N, int M, int K, int wpw, int wpb, int nblkx,
+    wg_batch b, KParams kp, const float *__restrict__ action, int action_cols, int action_stride, KOut o, LeanGeo lg) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    b.pos = pos; b.vel = vel; b.edges = edges; b.inc = inc; b.N = N; b.M = M; b.K = K;
+    lg.nblk = nblkx & 0x3fffffff; lg.wpw = wpw; lg.wpb = wpb;
+    kp.prio = (int)((unsigned)nblkx >> 31);
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int bid = blockIdx.x, xb = xcd_block(bid, lg.nblk);
+    const int blk = (nblkx & 0x40000000) ? xb : bid;
+    const int tile = blk * lg.wpb + wv;
+    if (tile * lg.wpw >= b.N) return;
+#ifdef WG_STAMPS
+    const int stamp_wave = tile;
+#endif
+    STAMP(0);
+    const LeanTile t = lean_tile_of(b, action, action_cols, lg, tile, lane);
+    LeanIn<1> L;
+    if (kp.prio) __builtin_amdgcn_s_setprio(2);
+    lean_load<1>(b, kp, action, action_stride, t, lane, L);
+    if (kp.prio) __builtin_amdgcn_s_setprio(0);
+    STAMP(1);
+    lean_compute<IN3D, 1>(b, kp, o, lg, smem + wv * lg.slice, t, lane, L);
+}
+#endif
 
 // n_steps env steps in one launch (wg_rollout): the tile's static inputs (spring records, incidence lists, masses,
 // muscle bounds) are loaded once and its state (pos, vel, muscle x, step counter) stays in registers from step to
@@ -2665,6 +2729,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
     }
     if (!is_mus) { mx = 0.f; mlo = 0.f; mhi = 0.f; mst = 0.f; }
     if (!acts) act = 0.f;
+    // diverged walkers (lean_compute): every mass of the walker NaN somewhere in its position, unpinned, with a spring ->
+    // finite stand-ins now, NaN state and outputs after the integrator
+    bool dead = false;
+    if (!WG_AB_NODEAD) {
+        const bool dm = is_mass && pin == 0 && io1 > io0 &&
+                        (__builtin_isnan(p3[0]) || __builtin_isnan(p3[1]) || __builtin_isnan(p3[2]));
+        const unsigned long long db = __ballot(dm);
+        if (__builtin_expect(db != 0ull, 0)) {   // wave-uniform, rare
+            const int mwn = s_mo[mw + 1] - mlm;
+            const unsigned long long gm = (mwn >= 64) ? ~0ull : (((1ull << mwn) - 1ull) << mlm);
+            dead = is_mass && (db & gm) == gm;
+            if (dead) {
+                p3[0] = (float)(lane - mlm); p3[1] = 0.f; p3[2] = 0.f;
+                v3[0] = 0.f; v3[1] = 0.f; v3[2] = 0.f;
+            }
+        }
+    }
     if (kp.prio) __builtin_amdgcn_s_setprio(0);
     STAMP(1);
 
@@ -2727,6 +2808,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
         mass_accumulate_v2(ts, reinterpret_cast<const uint16_t *>(s_inc) + 2 * mlb, mlb, io0,
                            (WG_ABLATE & 2) ? min(io1, io0 + 1) : io1, mf, ym, ax, ay, az, wave_tiny);
         mass_tail(kp, mf, (float)ym, p3, v3, px, py, pz, vx, vy, vz, ax, ay, az, hit, pin != 0, &et);
+        if (dead) {
+            px = __builtin_nanf(""); py = px; pz = px; vx = px; vy = px; vz = px; ax = px; ay = px; az = px;
+            hit = false;
+        }
         const uint32_t pl = (uint32_t)(P0 + lane);
         float *gpo = WG_ST(b.pos, pl, 3), *gvo = WG_ST(b.vel, pl, 3), *gao = WG_ST(b.acc, pl, 3);
         gpo[0] = px; gpo[1] = py; gpo[2] = pz;
@@ -2745,7 +2830,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
         const float nv = nvm;
         s_tp[3 * lane] = px; s_tp[3 * lane + 1] = py; s_tp[3 * lane + 2] = pz;
         s_tn[lane] = nv;
-        s_tk[lane] = mf * np_sq(nv);   // p.m * norm(p.v) ** 2 (gym/optimized_env.py:242)
+        s_tk[lane] = dead ? nv : mf * np_sq(nv);   // p.m * norm(p.v) ** 2 (gym/optimized_env.py:242)
         s_te[lane] = (float)((double)mf * kp.g) * (py - kp.ground);
     }
     wave_sync();
@@ -3133,6 +3218,18 @@ int launch_lean(const wg_batch *b, const KParams &kp, bool in3d, const float *a,
         else if (ne == 4) WG_LAUNCH_LEAN(D3, 4);                               \
         else WG_LAUNCH_LEAN(D3, 8);                                            \
     } while (0)
+#if WG_AB_PRELOAD
+    if (ne <= 1) {
+        if (in3d)
+            hipLaunchKernelGGL((walker_step_lean_pre<true>), dim3(blocks), dim3(64 * g.wpb), lds, st, b->pos, b->vel,
+                               b->edges, b->inc, b->N, b->M, b->K, g.wpw, g.wpb, (int)((unsigned)g.nblk | ((unsigned)(kp.xcd & 2) << 29) | ((unsigned)(kp.prio != 0) << 31)), *b,
+                               kp, a, cols, astride, kout(o), g);
+        else
+            hipLaunchKernelGGL((walker_step_lean_pre<false>), dim3(blocks), dim3(64 * g.wpb), lds, st, b->pos, b->vel,
+                               b->edges, b->inc, b->N, b->M, b->K, g.wpw, g.wpb, (int)((unsigned)g.nblk | ((unsigned)(kp.xcd & 2) << 29) | ((unsigned)(kp.prio != 0) << 31)), *b,
+                               kp, a, cols, astride, kout(o), g);
+    } else
+#endif
     if (in3d) WG_LEAN_NE(true); else WG_LEAN_NE(false);
 #undef WG_LEAN_NE
 #undef WG_LAUNCH_LEAN

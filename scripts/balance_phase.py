@@ -8,6 +8,7 @@ import json
 import os
 import sys
 
+import numpy as np
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -21,14 +22,16 @@ def main():
     win = int(sys.argv[2]) if len(sys.argv) > 2 else 100
     scales = [float(x) for x in (sys.argv[3] if len(sys.argv) > 3 else "1,0").split(",")]
     n = int(os.environ.get("WG_N", "4096"))
-    out = {"walkers": n, "window": win, "runs": {}}
+    workload = os.environ.get("WG_WORKLOAD", "balance")   # (any bench.py workload: ragged for config 5)
+    out = {"workload": workload, "walkers": n, "window": win, "runs": {}}
     for s in scales:
-        spec, params = make_spec("balance", n, seed=1000)
+        spec, params = make_spec(workload, n, seed=1000)
         env = BatchedPhysicsEnv(spec, device="cuda:0", **params)
         g = torch.Generator(device="cuda:0").manual_seed(7)
         acts = ((torch.rand((steps, n, env.batch.A), generator=g, device="cuda:0") * 2 - 1) * s).contiguous()
         rows = []
-        wpw = env.launch_geometry()["walkers_per_block"]
+        wpw = env.launch_geometry()["walkers_per_block"]   # (-1 for wave tiles: walkers per wave vary)
+        wid = torch.as_tensor(np.repeat(np.arange(n), np.diff(np.asarray(spec["mass_off"]))), device="cuda:0")
         for w0 in range(0, steps, win):
             prep = env.prepare_run(acts[w0:w0 + win], win, lanes=1)
             torch.cuda.synchronize()
@@ -37,8 +40,9 @@ def main():
             prep()
             e1.record()
             torch.cuda.synchronize()
-            bad = ~torch.isfinite(env.pos).reshape(n, -1).all(1)
-            waves = bad.reshape(-1, wpw).any(1) if n % wpw == 0 else bad
+            badm = (~torch.isfinite(env.pos).all(1)).int()
+            bad = torch.zeros(n, dtype=torch.int32, device="cuda:0").index_put_((wid,), badm, accumulate=True) > 0
+            waves = bad.reshape(-1, wpw).any(1) if wpw > 0 and n % wpw == 0 else bad
             rows.append({"steps": [w0, w0 + win], "us_per_step": round(e0.elapsed_time(e1) / win * 1e3, 3),
                          "nonfinite_walkers": int(bad.sum()), "waves_with_nonfinite": int(waves.sum()),
                          "waves": int(waves.numel())})

@@ -8,7 +8,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
-       "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-gpu-flush-denormals-to-zero", "--cuda-device-only", "-c",
+       "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-gpu-flush-denormals-to-zero", "-mllvm",
+       "-amdgpu-kernarg-preload-count=10", "--cuda-device-only", "-c",
        "-Rpass-analysis=kernel-resource-usage", "-I", os.path.join(ROOT, "include"), "-o", "/dev/null", *sys.argv[1:],
        os.path.join(ROOT, "walker_gym_amd", "csrc", "walker_hip.hip")]
 out = subprocess.run(cmd, capture_output=True, text=True).stderr

@@ -4,7 +4,7 @@ while a walker only partly NaN, or with infinities, pinned masses or pair forces
 against the C oracle (the reference restated; pinned to the reference's own fixtures, two of which diverge: box 3D at
 step 38 and info_extras at step 27), bit for bit with NaN == NaN whatever the payload, on the lean kernel (canonical
 NE = 3, Balance-v0 2D NE = 1), the wave kernel (mixed topology) and the workgroup kernel (M = 25 without the wave
-plan), plus the resident rollout (no stand-in path) against per-step launches."""
+plan), plus the resident rollout (the stand-in path in its NE = 1 instance only) against per-step launches."""
 import numpy as np
 import pytest
 
@@ -123,14 +123,21 @@ def test_diverged_workgroup_kernel():
     _compare(spec, dict(in3d=1, pair_mode=3), 3, 9)
 
 
-def test_diverged_resident_rollout_equals_steps():
-    """The resident rollout (no stand-in path) and per-step launches (stand-in path) agree on diverged walkers."""
+@pytest.mark.parametrize("workload", ["canonical", "balance"])
+def test_diverged_resident_rollout_equals_steps(workload):
+    """The resident rollout and per-step launches agree on diverged walkers: canonical (NE = 3: the resident kernel has
+    no stand-in path) and Balance-v0 (NE = 1: both have it)."""
     import torch
     from walker_gym_amd.batched_env import BatchedPhysicsEnv
     from walker_gym_amd.synthetic import canonical_walkers
-    spec = _diverge(canonical_walkers(1024, seed=31), np.random.default_rng(6), pin=False)
-    a, b = BatchedPhysicsEnv(spec, in3d=1), BatchedPhysicsEnv(spec, in3d=1)
-    acts = (torch.rand((12, 1024, 8), device=a.device) * 2 - 1).contiguous()
+    from walker_gym_amd.walker import balance_spec
+    if workload == "canonical":
+        spec, kw = _diverge(canonical_walkers(1024, seed=31), np.random.default_rng(6), pin=False), dict(in3d=1)
+    else:
+        spec, kw = _diverge(balance_spec(2048), np.random.default_rng(7), n_dead=150, pin=False), dict(in3d=0)
+    a, b = BatchedPhysicsEnv(spec, **kw), BatchedPhysicsEnv(spec, **kw)
+    assert a.resident_ok()
+    acts = (torch.rand((12, a.N, a.batch.A), device=a.device) * 2 - 1).contiguous()
     ro = a.rollout(acts, resident=True)
     rs = b.rollout(acts, resident=False)
     torch.cuda.synchronize()

@@ -6,6 +6,7 @@ Numerics-relevant flags (the kernel restates numpy's float semantics op by op):
   -ffp-contract=off                        no a*b+c -> fma fusion (numpy rounds every op)
   -fhip-fp32-correctly-rounded-divide-sqrt IEEE float32 '/' and sqrtf
   -fno-gpu-flush-denormals-to-zero         keep float32 denormals, as x86 SSE does
+and one performance flag: -mllvm -amdgpu-kernarg-preload-count=10 (walker_step_lean1's leading arguments in SGPRs).
 """
 from __future__ import annotations
 
@@ -25,6 +26,9 @@ ARCH = os.environ.get("WALKER_HIP_ARCH", "gfx950")
 
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
          "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-gpu-flush-denormals-to-zero",
+         # the NE = 1 step kernel's ten leading arguments preloaded into SGPRs by the dispatch (walker_step_lean1;
+         # kernels whose first argument is a struct get none)
+         "-mllvm", "-amdgpu-kernarg-preload-count=10",
          "-Wall", "-Wno-unused-function"]
 
 

@@ -55,12 +55,6 @@ constexpr int MAXT = 512;               // __launch_bounds__: workgroups are 64.
 #ifndef WG_ABLATE
 #define WG_ABLATE 0
 #endif
-#ifndef WG_AB_NODEAD   // TEMPORARY A/B (round 6): 1 = no diverged-walker stand-in path
-#define WG_AB_NODEAD 0
-#endif
-#ifndef WG_AB_PRELOAD  // TEMPORARY A/B (round 6): 1 = NE = 1 with preloaded leading kernel arguments
-#define WG_AB_PRELOAD 0
-#endif
 
 // Float32 constants derived from wg_params exactly where numpy rounds the Python scalars.
 struct KParams {
@@ -861,7 +855,8 @@ __device__ __forceinline__ void mass_accumulate_v2(const TermsAoS &ts, const uin
         for (int r = s0; r < s1; r += 2) {
             B = inc_term_at(tb, fb, eb);
             const uint32_t ea2 = p[2];
-            __builtin_amdgcn_sched_barrier(0);   // keep the reads above the arithmetic
+            __builtin_amdgcn_sched_barrier(0);   // keep the reads above the arithmetic (without, at NE = 1: +2.5 %,
+                                                 // profiles/r06h_ab_nosb_balance4096.json)
             acc_entry_v2(A, ea, md, ym, mf, ymf, ax, ay, az);
             if (r + 1 >= s1) break;
             A = inc_term_at(tb, fb, ea2);
@@ -2246,11 +2241,12 @@ __device__ __forceinline__ void lean_compute(const wg_batch &b, const KParams &k
     // and its state, outputs and sums are then set to what the reference computes: NaN (NaN payloads aside).  A
     // walker only partly NaN, or with an inf, steps exactly as before.  Pair passes keep the plain path.
     bool dead = false;
-    if (!RES && kp.pair_mode == 0 && !WG_AB_NODEAD) {
-        const bool dm = is_mass && !pin && L.io1 > L.io0 &&
-                        (__builtin_isnan(L.p3[0]) || __builtin_isnan(L.p3[1]) || __builtin_isnan(L.p3[2]));
-        const unsigned long long db = __ballot(dm);
-        if (__builtin_expect(db != 0ull, 0)) {   // wave-uniform, rare
+    if ((!RES || NE == 1) && kp.pair_mode == 0) {   // (the resident kernel: its latency-bound NE = 1 instance)
+        // (the common test reads the positions only, the first loads to land: the pin / incidence words are waited for
+        // only in the rare branch, so the springs do not start later)
+        const bool nanp = is_mass && (__builtin_isnan(L.p3[0]) || __builtin_isnan(L.p3[1]) || __builtin_isnan(L.p3[2]));
+        if (__builtin_expect(__ballot(nanp) != 0ull, 0)) {   // wave-uniform, rare
+            const unsigned long long db = __ballot(nanp && !pin && L.io1 > L.io0);
             const unsigned long long gm = (M == 64) ? ~0ull : (((1ull << M) - 1ull) << (lane & ~(M - 1)));
             dead = is_mass && (db & gm) == gm;
             if (dead) {
@@ -2468,24 +2464,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lean_waves(
     // the wave index as a wave-uniform (scalar) value: the tile's walker range and element bases are then SALU
     // products, not per-lane v_mul_lo_u32
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // NE = 1 (the latency-bound small batches): every kernel argument the tile's loads need, in SGPRs before anything
-    // else.  Left to the compiler they come in three dependent scalar rounds (the XCD-order arguments, then the batch
-    // shape after that arithmetic, then the array bases after the early exit) before the first vector load.
-    // Balance-4096, one launch per step, same box, 7 interleaved rounds (profiles/r06b_ab_balance4096_prologue.json):
-    // 5.01 us against 5.33 with round 5's prologue and 5.52 with the explicit workgroup count alone.  NE >= 2 keeps
-    // round 5's prologue instruction for instruction (the pinned bases would cost those instances 11 VGPRs, 67 -> 78
-    // at NE = 3).
-    int blk;
-    if (NE == 1) {
-        asm volatile("" ::"s"(b.N), "s"(b.M), "s"(b.K), "s"(b.A), "s"(b.pos), "s"(b.vel), "s"(b.edges), "s"(b.inc),
-                     "s"(b.inc_off), "s"(b.mass), "s"(b.steps), "s"(b.muscle_x), "s"(b.muscle_bounds), "s"(action),
-                     "s"(action_stride), "s"(action_cols), "s"(kp.prio), "s"(kp.xcd), "s"(lg.nblk), "s"(lg.wpb),
-                     "s"(lg.wpw));
-        const int bid = blockIdx.x, xb = xcd_block(bid, lg.nblk);   // (the workgroup count as an explicit argument)
-        blk = (kp.xcd & 2) ? xb : bid;
-    } else {
-        blk = (kp.xcd & 2) ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
-    }
+    const int blk = (kp.xcd & 2) ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     const int tile = blk * lg.wpb + wv;
     if (tile * lg.wpw >= b.N) return;
 #ifdef WG_STAMPS
@@ -2502,12 +2481,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lean_waves(
     lean_compute<IN3D, NE>(b, kp, o, lg, smem + wv * lg.slice, t, lane, L);
 }
 
-#if WG_AB_PRELOAD   // TEMPORARY A/B (round 6): NE = 1 with its leading arguments preloaded into SGPRs by the dispatch
-// (-mllvm -amdgpu-kernarg-preload-count=10 preloads leading pointer / scalar arguments only, <= 14 SGPRs: these ten,
-// everything the tile index and the first vector loads need; nblkx = the workgroup count | the XCD-order flag << 30 |
-// the load-phase priority flag << 31)
+// NE = 1, the latency-bound small batches (Balance-4096: 512 waves, one per SIMD, the launch as long as its slowest
+// wave's dependent chain): the lean step with its leading arguments PRELOADED into SGPRs by the dispatch (build.py:
+// -mllvm -amdgpu-kernarg-preload-count=10; the option preloads leading pointer / scalar arguments only, <= 14 SGPRs).
+// These ten are everything the tile index and the first vector loads (pos, vel, spring records, incidence words) need,
+// so those loads issue at the wave's first instructions while one scalar round fetches the rest; nblkx = the workgroup
+// count | the XCD-order flag << 30 | the load-phase priority flag << 31.  Left to the compiler, walker_step_lean's
+// by-value structs had cost three dependent scalar rounds before the first vector load.  Balance-4096, one launch per
+// step, same box, interleaved: round 5's prologue 5.33 us, the same arguments in one scalar round 5.01
+// (profiles/r06b_ab_balance4096_prologue.json), preloaded 2.5 % below that (profiles/r06e_ab_*).
 template <bool IN3D>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lean_waves(1)))) void walker_step_lean_pre(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lean_waves(1)))) void walker_step_lean1(
     float *pos, float *vel, const wg_edge *edges, const uint16_t *inc, int N, int M, int K, int wpw, int wpb, int nblkx,
     wg_batch b, KParams kp, const float *__restrict__ action, int action_cols, int action_stride, KOut o, LeanGeo lg) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -2531,7 +2515,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lean_waves(
     STAMP(1);
     lean_compute<IN3D, 1>(b, kp, o, lg, smem + wv * lg.slice, t, lane, L);
 }
-#endif
 
 // n_steps env steps in one launch (wg_rollout): the tile's static inputs (spring records, incidence lists, masses,
 // muscle bounds) are loaded once and its state (pos, vel, muscle x, step counter) stays in registers from step to
@@ -2732,11 +2715,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NE >= 8 ? 4
     // diverged walkers (lean_compute): every mass of the walker NaN somewhere in its position, unpinned, with a spring ->
     // finite stand-ins now, NaN state and outputs after the integrator
     bool dead = false;
-    if (!WG_AB_NODEAD) {
-        const bool dm = is_mass && pin == 0 && io1 > io0 &&
-                        (__builtin_isnan(p3[0]) || __builtin_isnan(p3[1]) || __builtin_isnan(p3[2]));
-        const unsigned long long db = __ballot(dm);
-        if (__builtin_expect(db != 0ull, 0)) {   // wave-uniform, rare
+    {
+        const bool nanp = is_mass && (__builtin_isnan(p3[0]) || __builtin_isnan(p3[1]) || __builtin_isnan(p3[2]));
+        if (__builtin_expect(__ballot(nanp) != 0ull, 0)) {   // wave-uniform, rare
+            const unsigned long long db = __ballot(nanp && pin == 0 && io1 > io0);
             const int mwn = s_mo[mw + 1] - mlm;
             const unsigned long long gm = (mwn >= 64) ? ~0ull : (((1ull << mwn) - 1ull) << mlm);
             dead = is_mass && (db & gm) == gm;
@@ -3212,25 +3194,25 @@ int launch_lean(const wg_batch *b, const KParams &kp, bool in3d, const float *a,
                        astride, kout(o), g)
 #define WG_LEAN_NE(D3)                                                         \
     do {                                                                       \
-        if (ne <= 1) WG_LAUNCH_LEAN(D3, 1);                                    \
-        else if (ne == 2) WG_LAUNCH_LEAN(D3, 2);                               \
+        if (ne == 2) WG_LAUNCH_LEAN(D3, 2);                                    \
         else if (ne == 3) WG_LAUNCH_LEAN(D3, 3);                               \
         else if (ne == 4) WG_LAUNCH_LEAN(D3, 4);                               \
         else WG_LAUNCH_LEAN(D3, 8);                                            \
     } while (0)
-#if WG_AB_PRELOAD
-    if (ne <= 1) {
+    if (ne <= 1) {   // (the NE = 1 entry with preloaded arguments)
         if (in3d)
-            hipLaunchKernelGGL((walker_step_lean_pre<true>), dim3(blocks), dim3(64 * g.wpb), lds, st, b->pos, b->vel,
+            hipLaunchKernelGGL((walker_step_lean1<true>), dim3(blocks), dim3(64 * g.wpb), lds, st, b->pos, b->vel,
                                b->edges, b->inc, b->N, b->M, b->K, g.wpw, g.wpb, (int)((unsigned)g.nblk | ((unsigned)(kp.xcd & 2) << 29) | ((unsigned)(kp.prio != 0) << 31)), *b,
                                kp, a, cols, astride, kout(o), g);
         else
-            hipLaunchKernelGGL((walker_step_lean_pre<false>), dim3(blocks), dim3(64 * g.wpb), lds, st, b->pos, b->vel,
+            hipLaunchKernelGGL((walker_step_lean1<false>), dim3(blocks), dim3(64 * g.wpb), lds, st, b->pos, b->vel,
                                b->edges, b->inc, b->N, b->M, b->K, g.wpw, g.wpb, (int)((unsigned)g.nblk | ((unsigned)(kp.xcd & 2) << 29) | ((unsigned)(kp.prio != 0) << 31)), *b,
                                kp, a, cols, astride, kout(o), g);
-    } else
-#endif
-    if (in3d) WG_LEAN_NE(true); else WG_LEAN_NE(false);
+    } else if (in3d) {
+        WG_LEAN_NE(true);
+    } else {
+        WG_LEAN_NE(false);
+    }
 #undef WG_LEAN_NE
 #undef WG_LAUNCH_LEAN
     const hipError_t e = hipGetLastError();

@@ -15,7 +15,7 @@ every walker takes every step, and one range's next step fills the GPU while the
 (state, topology and a distinct U(-1,1) action tensor for every timed step) are resident in HBM before timing.
 Weak scaling: each rank owns its own `--walkers` walkers (no data-path collective).  Inside a torch.distributed world
 RCCL's communicator is created before the env's warm-up and checked (`comm`: its size by an all_reduce of ones, every
-rank's device and PCI address distinct), the job time is max(t1) - min(t0) over ranks on the node's shared clock, and
+rank's PCI address distinct), the job time is max(t1) - min(t0) over ranks on the node's shared clock, and
 the rollout-end gather (RCCL all_gather_into_tensor of the final observations and the per-step reward / done records)
 runs after the barrier that closes the K timed steps (`--gather serial`, the default): `value` is the K steps,
 `value_incl_gather` the steps and the gather, and `gather.content_check` compares every rank's checksums of what it
@@ -307,8 +307,8 @@ class DistPlumbing:
 
 def comm_report(pg: "DistPlumbing", world: int, identity: dict, strict: bool) -> dict:
     """The line's `comm` block: the communicator's size (must equal the world), every rank's device
-    and PCI address (must be distinct when strict, i.e. RCCL; a gloo rehearsal may share one GPU).  A failed check ends
-    the run with exit status 3 on every rank."""
+    and PCI address (the PCI addresses must be distinct when strict, i.e. RCCL; a gloo rehearsal may share one
+    GPU; device indices may repeat under per-rank visibility).  A failed check ends the run with exit status 3 on every rank."""
     size = pg.comm_size()
     ids = pg.all_objects(identity)
     from walker_gym_amd.distributed import check_distinct

@@ -99,7 +99,8 @@ def test_shared_device_exits_3():
 def test_check_distinct():
     from walker_gym_amd.distributed import check_distinct
     assert check_distinct([{"device": 0, "pci": "0000:05:00"}, {"device": 1, "pci": "0000:06:00"}]) == (True, "")
-    assert not check_distinct([{"device": 0, "pci": "0000:05:00"}, {"device": 0, "pci": "0000:06:00"}])[0]
+    # per-rank device visibility: every rank's GPU is its index 0, the PCI addresses still tell them apart
+    assert check_distinct([{"device": 0, "pci": "0000:05:00"}, {"device": 0, "pci": "0000:06:00"}])[0]
     assert not check_distinct([{"device": 0, "pci": "0000:05:00"}, {"device": 1, "pci": "0000:05:00"}])[0]
 
 

@@ -95,6 +95,16 @@ def test_errors_without_gpu(lib):
     assert lib.wg_step_simple(C.byref(rb), None, C.byref(p), 1, None) == _lib.WG_EINVAL
     assert b"uniform batches only" in lib.wg_last_error()
     assert lib.wg_observe_simple(C.byref(rb), C.byref(p), None, None, None, None, None, None) == _lib.WG_EINVAL
+    # the measurement aid (ABI 14): an output pointer and n_steps >= 1 required, the batch checked as wg_step checks it
+    ms = C.c_float(-1.0)
+    assert lib.wg_time_step(None, C.byref(p), None, 0, 0, 0, None, 1, None, 0, None, C.byref(ms)) == _lib.WG_EINVAL
+    assert b"ms_per_launch" in lib.wg_last_error() or b"null batch" in lib.wg_last_error()
+    ub = _lib.WgBatch(N=4, M=8, K=4, A=0)
+    assert lib.wg_time_step(C.byref(ub), C.byref(p), None, 0, 0, 0, None, 0, None, 0, None, C.byref(ms)) == _lib.WG_EINVAL
+    assert lib.wg_time_step(C.byref(ub), C.byref(p), None, 0, 0, 0, None, 1, None, 0, None, None) == _lib.WG_EINVAL
+    assert b"ms_per_launch" in lib.wg_last_error()
+    assert lib.wg_time_step(C.byref(ub), C.byref(p), None, 0, 0, 0, None, 1, None, 0, None, C.byref(ms)) == _lib.WG_EINVAL
+    assert b"missing state pointer" in lib.wg_last_error() and ms.value == -1.0
     # pair passes need the engine.py spring (spring_mode 0): refused before any launch
     b = _lib.WgBatch(N=4, M=8, K=4, A=0, ragged=1)
     for f in ("pos", "vel", "acc", "mass", "edges", "inc", "inc_off", "muscle_x", "steps", "mass_off", "edge_off",

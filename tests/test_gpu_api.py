@@ -169,3 +169,30 @@ def test_survey_signature_entry_points_bit_exact(workload):
     r_env = BatchedPhysicsEnv(ragged_walkers(64, seed=2, mmin=4, mmax=12), device="cuda:0", in3d=1)
     assert L.wg_step_simple(C.byref(r_env.batch.struct), None, C.byref(r_env._pstruct), 1, st) == _lib.WG_EINVAL
     assert b"uniform batches only" in L.wg_last_error()
+
+
+@pytest.mark.parametrize("workload", ["canonical", "ragged", "balance2d", "chain"])
+def test_time_launches_steps_as_run(workload):
+    """wg_time_step (ABI 14, bench.py's roofline): the same steps as run(lanes=1) — every step kernel (lean, wave, NE = 1
+    and workgroup kernels) launched through hipExtLaunchKernel with its own start / end events — bit-identical state
+    and outputs, and a positive mean kernel duration."""
+    import torch
+    from walker_gym_amd.batched_env import BatchedPhysicsEnv
+    from walker_gym_amd.synthetic import canonical_walkers, chain_walkers, ragged_walkers
+    from walker_gym_amd.walker import balance_spec
+    spec, kw = {"canonical": (canonical_walkers(640, seed=4), dict(in3d=1)),
+                "ragged": (ragged_walkers(300, seed=4, mmin=4, mmax=32), dict(in3d=1)),
+                "balance2d": (balance_spec(640), dict(in3d=0)),
+                "chain": (chain_walkers(40, 20, seed=4), dict(in3d=1, g=0.0, ground=-1.0e6, pair_mode=1))}[workload]
+    a_env = BatchedPhysicsEnv(spec, device="cuda:0", **kw)
+    b_env = BatchedPhysicsEnv(spec, device="cuda:0", **kw)
+    T, N, A = 6, a_env.N, max(1, a_env.batch.A)
+    g = torch.Generator(device="cuda:0").manual_seed(9)
+    acts = (torch.rand((T, N, A), generator=g, device="cuda:0") * 2 - 1).contiguous()
+    a_env.run(acts, T, lanes=1)
+    ms = b_env.time_launches(acts, T)
+    torch.cuda.synchronize()
+    assert 0.0 < ms < 1000.0
+    bits = lambda t: t.contiguous().view(torch.int32) if t.dtype == torch.float32 else t
+    for name in ("pos", "vel", "acc", "muscle_x", "steps", "obs", "reward", "done", "centroid", "energy"):
+        assert torch.equal(bits(getattr(a_env, name)), bits(getattr(b_env, name))), name

@@ -13,7 +13,7 @@ import threading
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libwalker_hip.so"
 LIB_PATH = os.path.join(HERE, LIB_NAME)
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 WG_EINVAL, WG_ERANGE, WG_EHIP = -1, -2, -3
 
@@ -61,7 +61,7 @@ class WgLaunchInfo(C.Structure):
 
 EXPORTS = ("wg_abi_version", "wg_last_error", "wg_step", "wg_step_ranges", "wg_run_ranges", "wg_rollout", "wg_observe",
            "wg_step_simple", "wg_observe_simple", "wg_reset", "wg_reset_noise", "wg_plan_ragged", "wg_plan_waves",
-           "wg_wave_edge_passes", "wg_plan_errors", "wg_launch_geometry", "wg_launch_floor")
+           "wg_wave_edge_passes", "wg_plan_errors", "wg_launch_geometry", "wg_launch_floor", "wg_time_step")
 
 _lib = None
 _lock = threading.Lock()
@@ -104,6 +104,7 @@ def load(path: str | None = None):
         L.wg_plan_errors.argtypes = [C.c_int32]
         L.wg_launch_geometry.argtypes = [C.POINTER(WgBatch), C.POINTER(WgLaunchInfo)]
         L.wg_launch_floor.argtypes = [C.c_int32, C.c_int32, C.c_int32, _vp, _vp, C.c_int32, _vp]
+        L.wg_time_step.argtypes = L.wg_step.argtypes + [C.POINTER(C.c_float)]   # ABI 14, measurement aid
         for f in EXPORTS[2:]:
             getattr(L, f).restype = C.c_int
         v = L.wg_abi_version()

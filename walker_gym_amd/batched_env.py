@@ -531,6 +531,18 @@ class BatchedPhysicsEnv:
                 torch.cuda.current_stream(self.device).cuda_stream)
         return PreparedRun(self, entry, getattr(_lib.load(), entry), args, [o] + pins, steps_valid, stale)
 
+    def time_launches(self, actions, n_steps: int, info: bool = True) -> float:
+        """Measurement aid (bench.py's roofline): run(actions, n_steps, lanes=1)'s steps — one full-batch launch per
+        step, the same results — with each step kernel's own start and end stamped on events of its own (wg_time_step,
+        hipExtLaunchKernel: the dispatch's timestamps, as a kernel trace reports them, without the gaps between
+        back-to-back launches).  Waits for the calling stream; returns the mean kernel duration in ms."""
+        prep = self.prepare_run(actions, n_steps, info=info, lanes=1)
+        ms = C.c_float(0.0)
+        _lib.check(_lib.load().wg_time_step(*prep._args, C.byref(ms)), "wg_time_step")
+        self._steps_at = self.batch.version if prep._steps_valid else -1   # (as PreparedRun.__call__)
+        self._stale = prep._stale
+        return float(ms.value)
+
     def _lanes(self, lanes: Optional[int]) -> int:
         """Walker ranges run() steps on separate streams (ragged batches: ranges of plan blocks).  Default 2 for
         batches of >= 2^19 masses: measured on the canonical 65,536-walker bench (2^20 masses), 36.5 us/step

@@ -21,6 +21,7 @@
 // exactly as numpy's does.
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <cstdarg>
@@ -28,6 +29,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "walker_hip.h"
 #include "powf2.h"
@@ -92,6 +94,18 @@ inline KOut kout(const wg_outputs &o) {
     return KOut{o.obs, o.reward, o.done, o.centroid, o.energy, o.steps, o.obs_step, o.out_step, o.obs_stride,
                 o.obs_pad_clean};
 }
+
+// Step-kernel launches.  wg_time_step (ABI 14, a measurement aid) sets the two events on this thread around each step it
+// issues: the launch then goes through hipExtLaunchKernel, which stamps the kernel's own start and end on them (the
+// dispatch's timestamps, as a kernel trace reports them); otherwise a plain launch.
+thread_local hipEvent_t g_kev_start = nullptr, g_kev_stop = nullptr;
+#define WG_KLAUNCH(KERNEL, GRID, BLOCK, LDS, STREAM, ...)                                                          \
+    do {                                                                                                          \
+        if (g_kev_start)                                                                                          \
+            hipExtLaunchKernelGGL(KERNEL, GRID, BLOCK, LDS, STREAM, g_kev_start, g_kev_stop, 0u, __VA_ARGS__);    \
+        else                                                                                                      \
+            hipLaunchKernelGGL(KERNEL, GRID, BLOCK, LDS, STREAM, __VA_ARGS__);                                    \
+    } while (0)
 
 // XCD-aware workgroup order: MI355X deals workgroups round-robin over its 8 XCDs (each with its own L2; observed
 // placement, speed only), so hardware block b runs on XCD group b % 8.  The guide's bijective T1 swizzle maps b to a
@@ -3095,8 +3109,8 @@ int launch(const wg_batch *b, const KParams &kp, const float *action, int cols, 
     const int lds_static = (int)(sizeof(s_pw_log2) + sizeof(s_pw_exp2));
     if (g.lds + lds_static > LDS_LIMIT)
         return fail(WG_ERANGE, "workgroup needs %d B of LDS (> 160 KiB)", g.lds + lds_static);
-    hipLaunchKernelGGL((walker_step_kernel<STEP, RAGGED, IN3D, PWD, SHFL>), dim3(blocks), dim3(g.threads), g.lds, stream,
-                       *b, kp, action, cols, astride, kout(o), plan, g);
+    WG_KLAUNCH((walker_step_kernel<STEP, RAGGED, IN3D, PWD, SHFL>), dim3(blocks), dim3(g.threads), (uint32_t)g.lds, stream,
+               *b, kp, action, cols, astride, kout(o), plan, g);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(WG_EHIP, "launch failed: %s", hipGetErrorString(e));
     return 0;
@@ -3190,8 +3204,8 @@ int launch_lean(const wg_batch *b, const KParams &kp, bool in3d, const float *a,
     // WG_LDS_PAD (diagnostic): extra LDS bytes per workgroup, to measure the kernel at lower occupancy
     const int lds = g.wpb * g.slice + std::max(0, env_int("WG_LDS_PAD", 0));
 #define WG_LAUNCH_LEAN(D3, NE_)                                                                                  \
-    hipLaunchKernelGGL((walker_step_lean<D3, NE_>), dim3(blocks), dim3(64 * g.wpb), lds, st, *b, kp, a, cols,   \
-                       astride, kout(o), g)
+    WG_KLAUNCH((walker_step_lean<D3, NE_>), dim3(blocks), dim3(64 * g.wpb), (uint32_t)lds, st, *b, kp, a, cols,  \
+               astride, kout(o), g)
 #define WG_LEAN_NE(D3)                                                         \
     do {                                                                       \
         if (ne == 2) WG_LAUNCH_LEAN(D3, 2);                                    \
@@ -3201,11 +3215,11 @@ int launch_lean(const wg_batch *b, const KParams &kp, bool in3d, const float *a,
     } while (0)
     if (ne <= 1) {   // (the NE = 1 entry with preloaded arguments)
         if (in3d)
-            hipLaunchKernelGGL((walker_step_lean1<true>), dim3(blocks), dim3(64 * g.wpb), lds, st, b->pos, b->vel,
+            WG_KLAUNCH((walker_step_lean1<true>), dim3(blocks), dim3(64 * g.wpb), (uint32_t)lds, st, b->pos, b->vel,
                                b->edges, b->inc, b->N, b->M, b->K, g.wpw, g.wpb, (int)((unsigned)g.nblk | ((unsigned)(kp.xcd & 2) << 29) | ((unsigned)(kp.prio != 0) << 31)), *b,
                                kp, a, cols, astride, kout(o), g);
         else
-            hipLaunchKernelGGL((walker_step_lean1<false>), dim3(blocks), dim3(64 * g.wpb), lds, st, b->pos, b->vel,
+            WG_KLAUNCH((walker_step_lean1<false>), dim3(blocks), dim3(64 * g.wpb), (uint32_t)lds, st, b->pos, b->vel,
                                b->edges, b->inc, b->N, b->M, b->K, g.wpw, g.wpb, (int)((unsigned)g.nblk | ((unsigned)(kp.xcd & 2) << 29) | ((unsigned)(kp.prio != 0) << 31)), *b,
                                kp, a, cols, astride, kout(o), g);
     } else if (in3d) {
@@ -3279,8 +3293,8 @@ int launch_waves(const wg_batch *b, const KParams &kp, bool in3d, const float *a
     const int blocks = (ntiles + g.wpb - 1) / g.wpb;
     const int lds = g.wpb * g.slice;
 #define WG_LAUNCH_WAVES(D3, NE_)                                                                                  \
-    hipLaunchKernelGGL((walker_step_waves<D3, NE_>), dim3(blocks), dim3(64 * g.wpb), lds, st, *b, kp, a, cols,    \
-                       astride, kout(o), plan, ntiles, g)
+    WG_KLAUNCH((walker_step_waves<D3, NE_>), dim3(blocks), dim3(64 * g.wpb), (uint32_t)lds, st, *b, kp, a, cols,   \
+               astride, kout(o), plan, ntiles, g)
 #define WG_WAVES_NE(D3)                                                        \
     do {                                                                       \
         if (ne <= 1) WG_LAUNCH_WAVES(D3, 1);                                   \
@@ -3488,6 +3502,40 @@ int wg_observe_simple(const wg_batch *b, const wg_obs_cfg *cfg, float *obs, floa
     o.centroid = centroid;
     o.energy = energy;
     return run(b, cfg, nullptr, 0, 0, 0, &o, 1, nullptr, 0, stream, false);
+}
+
+// ABI 14, a measurement aid (bench.py's roofline): wg_step's n_steps, one launch per step, each step kernel launched with
+// a start and an end event of its own (hipExtLaunchKernel: the dispatch's own timestamps, so the launch gaps of
+// back-to-back launches are not counted); waits for the stream, then *ms_per_launch = the mean kernel duration.
+int wg_time_step(const wg_batch *b, const wg_params *p, const float *action, int32_t action_cols, int32_t action_stride,
+                 int64_t action_step, const wg_outputs *o, int32_t n_steps, const int32_t *plan, int32_t plan_blocks,
+                 hipStream_t stream, float *ms_per_launch) {
+    if (!ms_per_launch || n_steps < 1) return fail(WG_EINVAL, "wg_time_step: n_steps >= 1 and ms_per_launch required");
+    int rc = run(b, p, action, action_cols, action_stride, action_step, o, n_steps, plan, plan_blocks, stream, true,
+                 false, true);   // every argument checked before the first launch
+    if (rc) return rc;
+    if (b->N == 0) return fail(WG_EINVAL, "wg_time_step: empty batch (no launch to time)");
+    std::vector<hipEvent_t> ev((size_t)2 * n_steps, nullptr);
+    for (auto &e : ev)
+        if (hipEventCreate(&e) != hipSuccess) { rc = fail(WG_EHIP, "wg_time_step: event create failed"); break; }
+    for (int s = 0; s < n_steps && !rc; s++) {
+        g_kev_start = ev[2 * s]; g_kev_stop = ev[2 * s + 1];
+        rc = run(b, p, action, action_cols, action_stride, action_step, o, 1, plan, plan_blocks, stream, true, false,
+                 false, s);
+    }
+    g_kev_start = g_kev_stop = nullptr;
+    double total = 0.0;
+    if (!rc && hipStreamSynchronize(stream) != hipSuccess) rc = fail(WG_EHIP, "wg_time_step: stream sync failed");
+    for (int s = 0; s < n_steps && !rc; s++) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, ev[2 * s], ev[2 * s + 1]) != hipSuccess)
+            rc = fail(WG_EHIP, "wg_time_step: elapsed time of step %d unavailable", s);
+        total += ms;
+    }
+    for (auto e : ev)
+        if (e) (void)hipEventDestroy(e);
+    if (!rc) *ms_per_launch = (float)(total / n_steps);
+    return rc;
 }
 
 int wg_reset(const wg_batch *b, const wg_params *p, const float *noise, const uint8_t *mask, hipStream_t stream) {

@@ -3525,7 +3525,8 @@ int wg_time_step(const wg_batch *b, const wg_params *p, const float *action, int
     }
     g_kev_start = g_kev_stop = nullptr;
     double total = 0.0;
-    if (!rc && hipStreamSynchronize(stream) != hipSuccess) rc = fail(WG_EHIP, "wg_time_step: stream sync failed");
+    // (after a failure part-way, the launches already issued still hold their events: wait for them before destroying)
+    if (hipStreamSynchronize(stream) != hipSuccess && !rc) rc = fail(WG_EHIP, "wg_time_step: stream sync failed");
     for (int s = 0; s < n_steps && !rc; s++) {
         float ms = 0.f;
         if (hipEventElapsedTime(&ms, ev[2 * s], ev[2 * s + 1]) != hipSuccess)
